@@ -1,0 +1,58 @@
+# Build of the MI355X (gfx950) Viterbi engine, its oracle and the C++ parity tests.
+# `make -j16` (the GPU box allows at most -j16).  __graft_entry__.build() runs this.
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+CC       ?= gcc
+ARCH     ?= gfx950
+REF      ?= /root/reference
+
+CSRC     := spec_viterbi_amd/csrc
+BUILD    := build
+LIB      := spec_viterbi_amd/libspec_viterbi_hip.so
+ORACLE   := oracle/liboracle.so
+
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) \
+            -fno-honor-nans -mllvm -amdgpu-atomic-optimizer-strategy=None -Wall -Wno-unused-parameter
+HOSTFLAGS := --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall
+
+HIP_SRCS  := $(wildcard $(CSRC)/fused_*.hip) $(CSRC)/misc.hip
+HOST_SRCS := $(CSRC)/runtime.cpp $(CSRC)/svh_api.cpp $(CSRC)/HIP_impl.cpp $(CSRC)/data_reader.cpp
+OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS))
+HDRS := $(wildcard $(CSRC)/*.h) $(wildcard include/*.h)
+
+CPP_TESTS := tests/cpp/test_HIP_impl tests/cpp/test_HIP_spec_impl tests/cpp/test_semantic_equality
+
+.PHONY: all lib oracle ref tests clean
+all: lib oracle tests ref
+
+lib: $(LIB)
+oracle: $(ORACLE)
+tests: $(CPP_TESTS)
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+$(BUILD)/%.o: $(CSRC)/%.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/%.o: $(CSRC)/%.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+# Oracle: plain C, every add rounded on its own (test infrastructure only).
+$(ORACLE): oracle/viterbi_oracle.c oracle/viterbi_oracle.h
+	$(CC) -O2 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -shared -o $@ oracle/viterbi_oracle.c
+
+# C++ tests written against the reference's interfaces (tests/cpp/*.cpp).
+tests/cpp/%: tests/cpp/%.cpp tests/cpp/test_helper.h $(LIB)
+	$(HIPCC) $(HOSTFLAGS) -o $@ $< -L$(dir $(LIB)) -lspec_viterbi_hip -Wl,-rpath,'$$ORIGIN/../../spec_viterbi_amd'
+
+# The reference's own reader, compiled from its sources where they lie (oracle/_ref only).
+ref:
+	@if [ -f $(REF)/Viterbi_impl/data_reader.cpp ]; then $(MAKE) -C oracle -f ref.mk REF=$(REF); \
+	else echo "reference checkout not present: skipping oracle/_ref"; fi
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(ORACLE) $(CPP_TESTS) oracle/_ref

@@ -1,0 +1,135 @@
+/*
+ * svh.h -- C ABI of the MI355X (gfx950) Viterbi engine, libspec_viterbi_hip.so.
+ *
+ * This is the drop-in boundary for the reference's hot path.  Every entry point names the
+ * reference interface it replaces (paths relative to the IvanTyulyandin/Spec_Viterbi checkout):
+ *
+ *   svh_hmm_read / svh_hmm_*        read_HMM                        Viterbi_impl/data_reader.h:8
+ *   svh_ess_read / svh_ess_*        read_emit_seq                   Viterbi_impl/data_reader.h:11
+ *   svh_model_create                per-call model setup of GraphBLAS_impl::run_Viterbi
+ *                                   (GraphBLAS_impl.cpp:9-54), done once and kept in HBM
+ *   svh_viterbi / svh_batch_*       Viterbi_impl::run_Viterbi       Viterbi_impl/Viterbi_impl.h:8-9
+ *                                   (batched: one call = many sequences)
+ *   svh_spec_build                  Viterbi_spec_impl::spec_with    Viterbi_impl/Viterbi_spec_impl.h:11
+ *   svh_viterbi(level >= 1)         Viterbi_spec_impl::run_Viterbi_spec  Viterbi_spec_impl.h:13-14
+ *
+ * Conventions: plain pointers and sizes, no C++ or torch types; every call returns an int status
+ * (SVH_OK == 0); svh_last_error() gives a thread-local message for the last failure; host
+ * buffers are caller-owned and only borrowed during the call; indices and symbols are uint64_t
+ * (the reference's size_t HMM::Index_t / HMM::Emit_t); scores are -log2 probabilities (fp32,
+ * +inf = impossible), bit-identical to GraphBLAS_impl.  Handles are thread-safe.
+ * A `stream` argument is a hipStream_t (NULL = the handle's own stream).
+ */
+#ifndef SPEC_VITERBI_SVH_H
+#define SPEC_VITERBI_SVH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVH_ABI_VERSION 1
+
+enum {
+    SVH_OK = 0,
+    SVH_E_INVALID = -1,     /* bad argument (null pointer, empty sequence, ...) */
+    SVH_E_RANGE = -2,       /* state index or symbol out of range */
+    SVH_E_NOMEM = -3,       /* host or device allocation failed */
+    SVH_E_HIP = -4,         /* HIP runtime error (no device, launch failure, ...) */
+    SVH_E_UNSUPPORTED = -5, /* valid request this build does not implement */
+    SVH_E_STATE = -6,       /* e.g. run at spec level L before svh_spec_build(L) */
+    SVH_E_IO = -7           /* file could not be opened / parsed */
+};
+
+typedef struct svh_hmm* svh_hmm_t;
+typedef struct svh_ess* svh_ess_t;
+typedef struct svh_model* svh_model_t;
+typedef struct svh_batch* svh_batch_t;
+
+int svh_abi_version(void);
+const char* svh_last_error(void);
+int svh_device_count(int* count);
+
+/* ---- readers (host; same parse and error semantics as data_reader.cpp) ------------------ */
+int svh_hmm_read(const char* path, svh_hmm_t* out);
+int svh_hmm_dims(svh_hmm_t h, uint64_t* n, uint64_t* S, uint64_t* nstart, uint64_t* ntrans);
+int svh_hmm_copy(svh_hmm_t h, uint64_t* start_cols, float* start_vals, float* emissions,
+                 uint64_t* trans_src, uint64_t* trans_dst, float* trans_prob);
+void svh_hmm_free(svh_hmm_t h);
+int svh_ess_read(const char* path, svh_ess_t* out);
+int svh_ess_dims(svh_ess_t e, uint64_t* nseq, uint64_t* total_symbols);
+int svh_ess_copy(svh_ess_t e, uint64_t* offsets /* nseq + 1 */, uint64_t* symbols);
+void svh_ess_free(svh_ess_t e);
+
+/* ---- model: HMM resident in HBM -------------------------------------------------------- */
+enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2 };
+
+typedef struct {
+    int32_t device;      /* HIP device ordinal; -1 = the caller's current device */
+    int32_t kernel;      /* SVH_KERNEL_* */
+    int32_t max_threads; /* fused-kernel workgroup size cap (64..512, multiple of 64); 0 = 512 */
+    int32_t reserved;
+} svh_model_opts;
+
+/* emissions: S x n, symbol-major (HMM::emissions[symbol][state]); transitions as COO
+ * src -> dst (HMM::trans_rows / trans_cols / trans_probs); duplicates: first one wins
+ * (GrB_FIRST_FP32, GraphBLAS_impl.cpp:42-44). */
+int svh_model_create(uint64_t n, uint64_t S, uint64_t nstart, const uint64_t* start_cols,
+                     const float* start_vals, const float* emissions, uint64_t ntrans,
+                     const uint64_t* trans_src, const uint64_t* trans_dst,
+                     const float* trans_prob, const svh_model_opts* opts, svh_model_t* out);
+int svh_model_destroy(svh_model_t m);
+
+typedef struct {
+    int32_t kernel;        /* SVH_KERNEL_FUSED or SVH_KERNEL_GENERIC (what runs) */
+    int32_t family;        /* fused family id (0: R2 uniform-heavy, 1: R2, 2: R4, 3: R8, 4: R16) */
+    int32_t threads;       /* workgroup size */
+    int32_t slots;         /* states per thread */
+    int32_t light_terms;   /* R */
+    int32_t heavy_rows;    /* H */
+    int32_t heavy_uniform; /* 1 if heavy rows use the shared dominant-weight reduction */
+    int32_t device;
+    uint64_t n, S, nnz;
+    uint64_t lds_bytes;
+    uint64_t spec_level;   /* level of the products built by svh_spec_build (0/1: none needed) */
+    uint64_t spec_bytes;   /* HBM held by the products */
+} svh_model_info;
+int svh_model_get_info(svh_model_t m, svh_model_info* info);
+
+/* ---- _spec: precomputed products of `level` consecutive observations ------------------- */
+/* level <= 1: nothing to precompute (the fused kernel folds diag(E_o) (x) T^T on the fly,
+ * bit-identical to GraphBLAS_spec_impl level 1).  level >= 2: builds the S^level dense
+ * n x n products H[(k1..kL)] = M_kL (x) ... (x) M_k1 in HBM (GraphBLAS_spec_impl.cpp:15-36,
+ * 146-181).  Replaces any previous products. */
+int svh_spec_build(svh_model_t m, uint32_t level, void* stream);
+
+/* ---- batches: sequences resident in HBM ------------------------------------------------ */
+enum { SVH_BATCH_PATHS = 1 };
+
+/* offsets: nseq + 1 prefix offsets into symbols; every sequence must be non-empty. */
+int svh_batch_create(svh_model_t m, uint64_t nseq, const uint64_t* offsets,
+                     const uint64_t* symbols, uint32_t flags, svh_batch_t* out);
+/* Enqueue one pass over the batch on `stream` (asynchronous).  level 0 = GraphBLAS_impl
+ * semantics; level 1 = identical; level >= 2 = GraphBLAS_spec_impl(level) semantics (needs
+ * svh_spec_build(level)).  Paths need level <= 1 and SVH_BATCH_PATHS. */
+int svh_batch_run(svh_batch_t b, uint32_t level, void* stream);
+/* Synchronise `stream` and copy results to host (any pointer may be NULL). */
+int svh_batch_read(svh_batch_t b, void* stream, float* scores /* nseq * n */,
+                   int64_t* best_state /* nseq */, int32_t* paths /* offsets[nseq] */);
+/* Device pointers of the results (for device-side gathers). */
+int svh_batch_device_results(svh_batch_t b, float** scores, int64_t** best_state);
+/* Milliseconds between the start and stop events of the last svh_batch_run (synchronises). */
+int svh_batch_elapsed_ms(svh_batch_t b, float* ms);
+int svh_batch_destroy(svh_batch_t b);
+
+/* ---- one-shot convenience: upload, run, download --------------------------------------- */
+int svh_viterbi(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* offsets,
+                const uint64_t* symbols, float* scores, int64_t* best_state, int32_t* paths);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

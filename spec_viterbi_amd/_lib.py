@@ -1,0 +1,109 @@
+"""ctypes binding of the C ABI in include/svh.h (libspec_viterbi_hip.so, built in-tree).
+
+The product path has no fallback: if the HIP library is missing this module raises at import
+time, loudly, instead of silently computing on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+
+LIB_NAME = "libspec_viterbi_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+SVH_OK = 0
+SVH_E_INVALID = -1
+SVH_E_RANGE = -2
+SVH_E_NOMEM = -3
+SVH_E_HIP = -4
+SVH_E_UNSUPPORTED = -5
+SVH_E_STATE = -6
+SVH_E_IO = -7
+
+SVH_KERNEL_AUTO = 0
+SVH_KERNEL_FUSED = 1
+SVH_KERNEL_GENERIC = 2
+SVH_BATCH_PATHS = 1
+
+
+class SvhError(RuntimeError):
+    """Non-zero status from the C ABI; `code` is the SVH_E_* value."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"svh error {code}: {msg}")
+        self.code = code
+
+
+class svh_model_opts(ctypes.Structure):
+    _fields_ = [("device", c_int32), ("kernel", c_int32), ("max_threads", c_int32), ("reserved", c_int32)]
+
+
+class svh_model_info(ctypes.Structure):
+    _fields_ = [
+        ("kernel", c_int32), ("family", c_int32), ("threads", c_int32), ("slots", c_int32),
+        ("light_terms", c_int32), ("heavy_rows", c_int32), ("heavy_uniform", c_int32), ("device", c_int32),
+        ("n", c_uint64), ("S", c_uint64), ("nnz", c_uint64), ("lds_bytes", c_uint64),
+        ("spec_level", c_uint64), ("spec_bytes", c_uint64),
+    ]
+
+
+P_u64 = POINTER(c_uint64)
+P_f32 = POINTER(c_float)
+P_i64 = POINTER(c_int64)
+P_i32 = POINTER(c_int32)
+
+# name -> (restype, argtypes); every function declared in include/svh.h.
+SIGNATURES = {
+    "svh_abi_version": (c_int, []),
+    "svh_last_error": (c_char_p, []),
+    "svh_device_count": (c_int, [P_i32]),
+    "svh_hmm_read": (c_int, [c_char_p, POINTER(c_void_p)]),
+    "svh_hmm_dims": (c_int, [c_void_p, P_u64, P_u64, P_u64, P_u64]),
+    "svh_hmm_copy": (c_int, [c_void_p, P_u64, P_f32, P_f32, P_u64, P_u64, P_f32]),
+    "svh_hmm_free": (None, [c_void_p]),
+    "svh_ess_read": (c_int, [c_char_p, POINTER(c_void_p)]),
+    "svh_ess_dims": (c_int, [c_void_p, P_u64, P_u64]),
+    "svh_ess_copy": (c_int, [c_void_p, P_u64, P_u64]),
+    "svh_ess_free": (None, [c_void_p]),
+    "svh_model_create": (c_int, [c_uint64, c_uint64, c_uint64, P_u64, P_f32, P_f32, c_uint64, P_u64,
+                                 P_u64, P_f32, POINTER(svh_model_opts), POINTER(c_void_p)]),
+    "svh_model_destroy": (c_int, [c_void_p]),
+    "svh_model_get_info": (c_int, [c_void_p, POINTER(svh_model_info)]),
+    "svh_spec_build": (c_int, [c_void_p, c_uint32, c_void_p]),
+    "svh_batch_create": (c_int, [c_void_p, c_uint64, P_u64, P_u64, c_uint32, POINTER(c_void_p)]),
+    "svh_batch_run": (c_int, [c_void_p, c_uint32, c_void_p]),
+    "svh_batch_read": (c_int, [c_void_p, c_void_p, P_f32, P_i64, P_i32]),
+    "svh_batch_device_results": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
+    "svh_batch_elapsed_ms": (c_int, [c_void_p, P_f32]),
+    "svh_batch_destroy": (c_int, [c_void_p]),
+    "svh_viterbi": (c_int, [c_void_p, c_uint32, c_uint64, P_u64, P_u64, P_f32, P_i64, P_i32]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()' "
+            "or `make -j16`). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int) -> None:
+    if rc != SVH_OK:
+        msg = lib.svh_last_error()
+        raise SvhError(rc, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    c = c_int32(0)
+    check(lib.svh_device_count(ctypes.byref(c)))
+    return int(c.value)

@@ -1,0 +1,12 @@
+// Fused step kernel family: R=2 light terms per row, HM=2 heavy rows, XM=2 exceptions,
+// heavy mode kHeavyGeneral.  One family per translation unit so instantiations compile in parallel.
+#include "fused_impl.h"
+
+namespace svh {
+
+const void* fused_kernel_r2(int smax, bool paths) {
+    return paths ? fused_family_ptr<2, 2, 2, kHeavyGeneral, true>(smax)
+                 : fused_family_ptr<2, 2, 2, kHeavyGeneral, false>(smax);
+}
+
+}  // namespace svh

@@ -1,0 +1,145 @@
+// Internal interface between the host runtime (model.cpp) and the HIP kernels.
+// Not part of the public ABI (that is include/svh.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace svh {
+
+constexpr int kMaxHeavy = 4;      // heavy rows a fused-kernel family can hold
+constexpr int kMaxExc = 4;        // exception terms per heavy row
+constexpr int kMaxWaves = 16;     // waves per workgroup (B <= 1024)
+constexpr uint32_t kNoPred = 0xFFFFu;
+constexpr uint32_t kSymChunk = 4096;  // symbols staged in LDS per refill
+constexpr uint32_t kSymPad = 64;      // zero bytes after every sequence in device memory
+constexpr int kMaxFusedThreads = 512;
+
+enum HeavyMode : int { kHeavyGeneral = 0, kHeavyUniform = 1 };
+
+// Register-resident schedule of the fused step kernel (built by Plan in model.cpp).
+//   State j of the model lives in slot s = j / B of thread t = j % B (strided, so a wave's LDS
+//   accesses to v are lane-consecutive and bank-conflict free).  LDS index space of one score
+//   buffer: [0, estride) states, estride = +inf scratch, estride+1+h = heavy row h.
+struct FusedModel {
+    const float* emis;      // [S][estride] fp32, +inf padding beyond n (+16 floats)
+    const float* start;     // [estride] dense start column, +inf where absent
+    const uint32_t* lcol;   // [(s*R + r)*B + t] light-row term source (LDS index)
+    const float* lval;      // [(s*R + r)*B + t] light-row term T^T value (+inf padding)
+    const float* hval;      // GENERAL: [(h*SM + s)*B + t] heavy-row T^T over own sources
+    const uint8_t* hvalid;  // GENERAL: same layout, 1 where T^T has the entry (paths)
+    const float* hmask;     // UNIFORM: [s*B + t] 0 if own source is in the shared set U, +inf
+    int hrow[kMaxHeavy];    // heavy row ids (dummies: estride)
+    float hw[kMaxHeavy];    // UNIFORM: dominant weight of heavy row h
+    uint32_t xk[kMaxHeavy][kMaxExc];  // exception term source (LDS index; scratch = none)
+    float xw[kMaxHeavy][kMaxExc];     // exception term weight (+inf = none)
+    uint32_t H;             // number of real heavy rows
+    uint32_t n;             // states
+    uint32_t S;             // symbols
+    uint32_t slots;         // SM: slots per thread (the kernel instantiation)
+    uint32_t estride;       // slots * B (>= n)
+    uint32_t vstride;       // floats per LDS score buffer (multiple of 4)
+    uint32_t B;             // threads per workgroup
+};
+
+// One batch of sequences.  Symbols are uint8; each sequence 16-byte aligned, kSymPad padded.
+struct FusedBatch {
+    const uint8_t* symbols;
+    const uint64_t* sym_off;   // [nseq] byte offset of sequence q
+    const uint32_t* begin;     // [nseq] first step to run (0: start from the start column)
+    const uint32_t* end;       // [nseq] sequence length (steps run: max(begin,1)..end-1)
+    const float* v_in;         // rows of initial scores when begin > 0
+    const uint32_t* v_in_row;  // [nseq] row of v_in for sequence q (stride n)
+    float* scores;             // [nseq][n] final scores
+    int64_t* best;             // [nseq] lowest-index argmin of final scores (nullable)
+    uint16_t* bp;              // backpointers (PATHS only)
+    const uint64_t* bp_off;    // [nseq] element offset of sequence q's (len-1) x n block
+    uint32_t nseq;
+};
+
+// CSR of T^T used by the generic kernel and the _spec precompute.
+struct CsrModel {
+    const float* emis;       // [S][n]
+    const float* start;      // [n]
+    const uint32_t* rowptr;  // [n + 1]
+    const uint32_t* col;     // [nnz]
+    const float* val;        // [nnz]
+    const uint32_t* row_of;  // [nnz] row of entry p
+    uint32_t n;
+    uint32_t S;
+    uint32_t nnz;
+};
+
+// Kernel families of the fused step kernel.
+enum FusedFamily : int {
+    kFamR2Uni = 0,  // R=2, HM=2, uniform heavy rows (MSV / HMMER-style models)
+    kFamR2 = 1,     // R=2, HM=2, general heavy rows
+    kFamR4 = 2,     // R=4, HM=4
+    kFamR8 = 3,     // R=8, HM=4
+    kFamR16 = 4,    // R=16, HM=4
+    kNumFamilies = 5
+};
+int family_rmax(int fam);
+int family_hmax(int fam);
+int family_xmax(int fam);
+int family_mode(int fam);
+constexpr int kSlotChoices[] = {1, 2, 3, 4, 5, 6, 8, 10, 12, 16};
+constexpr int kNumSlotChoices = 10;
+
+// Per-family kernel lookup (fused_r*.hip).
+const void* fused_kernel_r2uni(int smax, bool paths);
+const void* fused_kernel_r2(int smax, bool paths);
+const void* fused_kernel_r4(int smax, bool paths);
+const void* fused_kernel_r8(int smax, bool paths);
+const void* fused_kernel_r16(int smax, bool paths);
+
+// LDS bytes the fused kernel needs for (SM, B, vstride): 3 score buffers, 3 E-ring slots of
+// ceil(SM/4) 16-byte DMA rows, heavy keys, reduction scratch, symbol ring.
+inline size_t fused_lds_bytes_for(int sm, uint32_t B, uint32_t vstride) {
+    const size_t ndma = (size_t)(sm + 3) / 4;
+    return (3 * (size_t)vstride + 3 * ndma * B * 4) * sizeof(float) +
+           3 * kMaxHeavy * sizeof(uint64_t) + 2 * kMaxWaves * sizeof(float) + kSymChunk + 64 + 16;
+}
+inline size_t fused_lds_bytes(const FusedModel& m) {
+    return fused_lds_bytes_for((int)m.slots, m.B, m.vstride);
+}
+constexpr size_t kMaxLdsBytes = 160 * 1024;
+
+hipError_t launch_fused(const FusedModel& m, const FusedBatch& b, int fam, bool paths,
+                        hipStream_t stream);
+size_t generic_lds_bytes(uint32_t n);
+hipError_t launch_generic(const CsrModel& m, const FusedBatch& b, int threads, bool paths,
+                          hipStream_t stream);
+hipError_t launch_traceback(const FusedBatch& b, const uint64_t* path_off, int32_t* paths,
+                            uint32_t n, hipStream_t stream);
+
+// _spec precompute / run (reference: GraphBLAS_spec_impl.cpp:15-36, 50-97, 146-181).
+// Dense products are stored row-major with row stride pstride = round_up(n, 4) (+inf padding).
+// K2: mfold[p * S + i] = fl(E[i][row(p)] + val[p])   (M_i = diag(E_i) (x) T^T, per nnz)
+hipError_t launch_spec_fold(const CsrModel& m, float* mfold, hipStream_t stream);
+// Dense level-1 products H1[o][j][m] (+inf off-pattern).
+hipError_t launch_spec_densify(const CsrModel& m, const float* mfold, float* h1, uint32_t pstride,
+                               hipStream_t stream);
+// K3: H_new[kp * S + i][j][m] = min_p fl(M_i[j][p] + H_prev[kp][p][m]) for kp in [0, kprev).
+hipError_t launch_spec_extend(const CsrModel& m, const float* mfold, const float* h_prev,
+                              uint64_t kprev, float* h_new, uint32_t pstride, hipStream_t stream);
+// K4: one level-L chunk for every sequence with chunk < nchunks[q].
+struct SpecChunkBatch {
+    const uint8_t* symbols;
+    const uint64_t* sym_off;
+    const uint32_t* nchunks;
+    const float* v_src;  // [nseq][n]
+    float* v_dst;        // [nseq][n]
+    uint32_t nseq;
+    uint32_t level;
+    uint32_t chunk;
+};
+hipError_t launch_spec_chunk(const CsrModel& m, const float* products, const SpecChunkBatch& c,
+                             uint32_t pstride, hipStream_t stream);
+// v0[q][j] = fl(E[s0][j] + start[j]) for every sequence.
+hipError_t launch_first_step(const CsrModel& m, const uint8_t* symbols, const uint64_t* sym_off,
+                             uint32_t nseq, float* v, hipStream_t stream);
+
+}  // namespace svh

@@ -1,0 +1,641 @@
+// Host runtime: model canonicalisation, fused-kernel planning, HBM residency, batches and the
+// _spec product pipeline.  See DESIGN.md for the layouts.
+#include "runtime.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <numeric>
+
+namespace svh {
+
+namespace {
+
+constexpr float kInfH = std::numeric_limits<float>::infinity();
+
+uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
+
+uint32_t float_bits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+
+}  // namespace
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) {
+        throw Error(e == hipErrorOutOfMemory ? SVH_E_NOMEM : SVH_E_HIP,
+                    std::string(what) + ": " + hipGetErrorString(e));
+    }
+}
+
+DeviceGuard::DeviceGuard(int dev) {
+    hip_check(hipGetDevice(&prev), "hipGetDevice");
+    if (dev != prev) hip_check(hipSetDevice(dev), "hipSetDevice");
+}
+DeviceGuard::~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+}
+
+DeviceBuffer& DeviceBuffer::operator=(DeviceBuffer&& o) noexcept {
+    if (this != &o) {
+        if (ptr) (void)hipFree(ptr);
+        ptr = o.ptr;
+        bytes = o.bytes;
+        o.ptr = nullptr;
+        o.bytes = 0;
+    }
+    return *this;
+}
+DeviceBuffer::~DeviceBuffer() {
+    if (ptr) (void)hipFree(ptr);
+}
+void DeviceBuffer::alloc(size_t nbytes) {
+    if (ptr) {
+        (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    if (nbytes == 0) nbytes = 16;
+    hip_check(hipMalloc(&ptr, nbytes), "hipMalloc");
+    bytes = nbytes;
+}
+void DeviceBuffer::upload(const void* src, size_t nbytes, hipStream_t s) {
+    alloc(nbytes);
+    if (nbytes) hip_check(hipMemcpyAsync(ptr, src, nbytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+}
+
+// ------------------------------------------------------------------------------------------
+// Canonical host model.  Reference semantics (GraphBLAS_impl.cpp:9-45): the start column and
+// T^T are built with GrB_Matrix_build(..., GrB_FIRST_FP32): duplicates keep the first tuple.
+// ------------------------------------------------------------------------------------------
+HostModel build_host_model(uint64_t n, uint64_t S, uint64_t nstart, const uint64_t* start_cols,
+                           const float* start_vals, const float* emissions, uint64_t ntrans,
+                           const uint64_t* src, const uint64_t* dst, const float* prob) {
+    if (n == 0 || S == 0) throw Error(SVH_E_INVALID, "model needs states_num > 0 and emit_num > 0");
+    if (n >= (1ull << 31)) throw Error(SVH_E_UNSUPPORTED, "states_num must be < 2^31");
+    if (S > 256) throw Error(SVH_E_UNSUPPORTED, "emit_num must be <= 256 (uint8 symbols in HBM)");
+    if (ntrans >= (1ull << 32)) throw Error(SVH_E_UNSUPPORTED, "trans_num must be < 2^32");
+    if (!emissions || (nstart && (!start_cols || !start_vals)) || (ntrans && (!src || !dst || !prob)))
+        throw Error(SVH_E_INVALID, "null model array");
+    HostModel h;
+    h.n = (uint32_t)n;
+    h.S = (uint32_t)S;
+    h.start.assign(n, kInfH);
+    std::vector<uint8_t> seen(n, 0);
+    for (uint64_t i = 0; i < nstart; ++i) {
+        const uint64_t c = start_cols[i];
+        if (c >= n) throw Error(SVH_E_RANGE, "start state index out of range");
+        if (!seen[c]) {
+            h.start[c] = start_vals[i];
+            seen[c] = 1;
+        }
+    }
+    h.emis.assign(emissions, emissions + S * n);
+
+    struct Tri { uint32_t dst, src, order; };
+    std::vector<Tri> t(ntrans);
+    for (uint64_t e = 0; e < ntrans; ++e) {
+        if (src[e] >= n || dst[e] >= n) throw Error(SVH_E_RANGE, "transition state index out of range");
+        t[e] = {(uint32_t)dst[e], (uint32_t)src[e], (uint32_t)e};
+    }
+    std::sort(t.begin(), t.end(), [](const Tri& a, const Tri& b) {
+        if (a.dst != b.dst) return a.dst < b.dst;
+        if (a.src != b.src) return a.src < b.src;
+        return a.order < b.order;
+    });
+    h.rowptr.assign(n + 1, 0);
+    h.col.reserve(ntrans);
+    h.val.reserve(ntrans);
+    for (uint64_t e = 0; e < ntrans; ++e) {
+        if (e > 0 && t[e].dst == t[e - 1].dst && t[e].src == t[e - 1].src) continue;  // FIRST
+        h.col.push_back(t[e].src);
+        h.val.push_back(prob[t[e].order]);
+        h.rowptr[t[e].dst + 1]++;
+    }
+    for (uint32_t j = 0; j < h.n; ++j) h.rowptr[j + 1] += h.rowptr[j];
+    return h;
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused-kernel planning.
+// ------------------------------------------------------------------------------------------
+namespace {
+
+struct HeavyAnalysis {
+    bool ok = false;
+    std::vector<uint32_t> heavy;  // row ids
+};
+
+// Uniform-heavy analysis: every heavy row = {dominant weight w_h over a non-heavy source set U
+// shared by all heavy rows} + <= XM exception terms.
+bool analyse_uniform(const HostModel& hm, const std::vector<int>& hidx,
+                     const std::vector<uint32_t>& heavy, uint32_t XM, float* hw,
+                     std::vector<std::pair<uint32_t, float>>* exc, std::vector<uint32_t>* U) {
+    if (heavy.empty()) return false;
+    std::vector<uint32_t> first_u;
+    for (size_t h = 0; h < heavy.size(); ++h) {
+        const uint32_t j = heavy[h];
+        std::map<uint32_t, uint32_t> count;
+        for (uint32_t p = hm.rowptr[j]; p < hm.rowptr[j + 1]; ++p)
+            if (hidx[hm.col[p]] < 0) count[float_bits(hm.val[p])]++;
+        uint32_t best_bits = float_bits(kInfH), best_cnt = 0;
+        for (const auto& [bits, c] : count)
+            if (c > best_cnt) {
+                best_cnt = c;
+                best_bits = bits;
+            }
+        std::memcpy(&hw[h], &best_bits, 4);
+        std::vector<uint32_t> u;
+        exc[h].clear();
+        for (uint32_t p = hm.rowptr[j]; p < hm.rowptr[j + 1]; ++p) {
+            const uint32_t k = hm.col[p];
+            if (hidx[k] < 0 && best_cnt > 0 && float_bits(hm.val[p]) == best_bits) u.push_back(k);
+            else exc[h].push_back({k, hm.val[p]});
+        }
+        if (exc[h].size() > XM) return false;
+        if (h == 0) first_u = u;
+        else if (u != first_u) return false;
+    }
+    *U = first_u;
+    return true;
+}
+
+}  // namespace
+
+Plan make_plan(const HostModel& hm, int max_threads, bool allow_uniform) {
+    Plan plan;
+    const uint32_t n = hm.n;
+    if (max_threads <= 0) max_threads = kMaxFusedThreads;
+    max_threads = std::min(max_threads, kMaxFusedThreads);
+    std::vector<uint32_t> rowlen(n);
+    for (uint32_t j = 0; j < n; ++j) rowlen[j] = hm.rowptr[j + 1] - hm.rowptr[j];
+
+    for (int fam = 0; fam < kNumFamilies; ++fam) {
+        const uint32_t R = family_rmax(fam), HM = family_hmax(fam), XM = family_xmax(fam);
+        const int mode = family_mode(fam);
+        if (mode == kHeavyUniform && !allow_uniform) continue;
+        std::vector<uint32_t> heavy;
+        for (uint32_t j = 0; j < n; ++j)
+            if (rowlen[j] > R) heavy.push_back(j);
+        if (heavy.size() > HM) continue;
+        std::vector<int> hidx(n, -1);
+        for (size_t h = 0; h < heavy.size(); ++h) hidx[heavy[h]] = (int)h;
+
+        float hw[kMaxHeavy] = {kInfH, kInfH, kInfH, kInfH};
+        std::vector<std::pair<uint32_t, float>> exc[kMaxHeavy];
+        std::vector<uint32_t> U;
+        if (mode == kHeavyUniform) {
+            if (!analyse_uniform(hm, hidx, heavy, XM, hw, exc, &U)) continue;
+        } else {
+            // general: exceptions are the heavy sources of each heavy row
+            for (size_t h = 0; h < heavy.size(); ++h) {
+                const uint32_t j = heavy[h];
+                for (uint32_t p = hm.rowptr[j]; p < hm.rowptr[j + 1]; ++p)
+                    if (hidx[hm.col[p]] >= 0) exc[h].push_back({hm.col[p], hm.val[p]});
+                if (exc[h].size() > XM) return plan;  // cannot happen: <= H <= HM <= XM
+            }
+        }
+
+        // geometry: fewest slots per thread whose workgroup fits the cap and LDS
+        uint32_t SM = 0, B = 0, vstride = 0;
+        size_t lds = 0;
+        for (int c = 0; c < kNumSlotChoices; ++c) {
+            const uint32_t sm = kSlotChoices[c];
+            uint32_t b = round_up((n + sm - 1) / sm, 64);
+            if (b < 64) b = 64;
+            if (b > (uint32_t)max_threads) continue;
+            const uint32_t vs = round_up(sm * b + 1 + kMaxHeavy, 4);
+            const size_t l = fused_lds_bytes_for((int)sm, b, vs);
+            if (l > kMaxLdsBytes) continue;
+            SM = sm;
+            B = b;
+            vstride = vs;
+            lds = l;
+            break;
+        }
+        if (SM == 0) return plan;  // too large for the fused kernel: generic fallback
+
+        plan.fused = true;
+        plan.family = fam;
+        plan.B = B;
+        plan.SM = SM;
+        plan.R = R;
+        plan.HM = HM;
+        plan.XM = XM;
+        plan.H = (uint32_t)heavy.size();
+        plan.mode = mode;
+        plan.estride = SM * B;
+        plan.vstride = vstride;
+        plan.lds_bytes = lds;
+        const uint32_t est = plan.estride, scratch = est, hs0 = est + 1;
+        auto lds_index = [&](uint32_t k) { return hidx[k] >= 0 ? hs0 + (uint32_t)hidx[k] : k; };
+
+        for (uint32_t h = 0; h < kMaxHeavy; ++h) {
+            plan.hrow[h] = h < plan.H ? (int)heavy[h] : 0;  // dummies: any valid state
+            plan.hw[h] = (h < plan.H && mode == kHeavyUniform) ? hw[h] : kInfH;
+            for (uint32_t x = 0; x < kMaxExc; ++x) {
+                const bool ok = h < plan.H && x < exc[h].size();
+                plan.xk[h][x] = ok ? lds_index(exc[h][x].first) : scratch;
+                plan.xw[h][x] = ok ? exc[h][x].second : kInfH;
+            }
+        }
+        // light rows
+        plan.lcol.assign((size_t)SM * R * B, scratch);
+        plan.lval.assign((size_t)SM * R * B, kInfH);
+        for (uint32_t j = 0; j < n; ++j) {
+            if (hidx[j] >= 0) continue;
+            const uint32_t s = j / B, t = j % B;
+            uint32_t r = 0;
+            for (uint32_t p = hm.rowptr[j]; p < hm.rowptr[j + 1]; ++p, ++r) {
+                const size_t idx = ((size_t)s * R + r) * B + t;
+                plan.lcol[idx] = lds_index(hm.col[p]);
+                plan.lval[idx] = hm.val[p];
+            }
+        }
+        // heavy rows
+        if (mode == kHeavyUniform) {
+            plan.hmask.assign(est, kInfH);
+            for (uint32_t k : U) plan.hmask[k] = 0.0f;
+        } else {
+            plan.hval.assign((size_t)HM * SM * B, kInfH);
+            plan.hvalid.assign((size_t)HM * SM * B, 0);
+            for (uint32_t h = 0; h < plan.H; ++h) {
+                const uint32_t j = heavy[h];
+                for (uint32_t p = hm.rowptr[j]; p < hm.rowptr[j + 1]; ++p) {
+                    const uint32_t k = hm.col[p];
+                    if (hidx[k] >= 0) continue;  // exception term
+                    const size_t idx = ((size_t)h * SM + k / B) * B + k % B;
+                    plan.hval[idx] = hm.val[p];
+                    plan.hvalid[idx] = 1;
+                }
+            }
+        }
+        // emissions padded to estride, plus the DMA over-read tail
+        const size_t ndma = (SM + 3) / 4;
+        plan.emis_pad.assign((size_t)hm.S * est + ndma * B * 4 + 64, kInfH);
+        for (uint32_t o = 0; o < hm.S; ++o)
+            std::copy(hm.emis.begin() + (size_t)o * n, hm.emis.begin() + (size_t)(o + 1) * n,
+                      plan.emis_pad.begin() + (size_t)o * est);
+        plan.start_pad.assign(est + 16, kInfH);
+        std::copy(hm.start.begin(), hm.start.end(), plan.start_pad.begin());
+        return plan;
+    }
+    return plan;
+}
+
+// ------------------------------------------------------------------------------------------
+// Model
+// ------------------------------------------------------------------------------------------
+void DevicePlan::upload(const Plan& p, hipStream_t s) {
+    plan = p;
+    if (!p.fused) return;
+    d_emis.upload(p.emis_pad.data(), p.emis_pad.size() * 4, s);
+    d_start.upload(p.start_pad.data(), p.start_pad.size() * 4, s);
+    d_lcol.upload(p.lcol.data(), p.lcol.size() * 4, s);
+    d_lval.upload(p.lval.data(), p.lval.size() * 4, s);
+    d_hval.upload(p.hval.data(), p.hval.size() * 4, s);
+    d_hvalid.upload(p.hvalid.data(), p.hvalid.size(), s);
+    d_hmask.upload(p.hmask.data(), p.hmask.size() * 4, s);
+    std::memset(&view, 0, sizeof(view));
+    view.emis = d_emis.as<float>();
+    view.start = d_start.as<float>();
+    view.lcol = d_lcol.as<uint32_t>();
+    view.lval = d_lval.as<float>();
+    view.hval = d_hval.as<float>();
+    view.hvalid = d_hvalid.as<uint8_t>();
+    view.hmask = d_hmask.as<float>();
+    for (int h = 0; h < kMaxHeavy; ++h) {
+        view.hrow[h] = p.hrow[h];
+        view.hw[h] = p.hw[h];
+        for (int x = 0; x < kMaxExc; ++x) {
+            view.xk[h][x] = p.xk[h][x];
+            view.xw[h][x] = p.xw[h][x];
+        }
+    }
+    view.H = p.H;
+    view.slots = p.SM;
+    view.estride = p.estride;
+    view.vstride = p.vstride;
+    view.B = p.B;
+}
+
+Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
+    int dev = opts ? opts->device : -1;
+    if (dev < 0) hip_check(hipGetDevice(&dev), "hipGetDevice");
+    device = dev;
+    kernel_pref = opts ? opts->kernel : SVH_KERNEL_AUTO;
+    const int max_threads = (opts && opts->max_threads > 0) ? opts->max_threads : kMaxFusedThreads;
+    if (max_threads % 64 != 0 || max_threads > kMaxFusedThreads)
+        throw Error(SVH_E_INVALID, "max_threads must be a multiple of 64 in [64, 512]");
+    DeviceGuard g(device);
+    hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+
+    Plan fast = make_plan(host, max_threads, true);
+    fast_plan.upload(fast, stream);
+    if (fast.fused) {
+        fast_plan.view.n = host.n;
+        fast_plan.view.S = host.S;
+    }
+    if (fast.fused && fast.mode == kHeavyUniform) {
+        Plan gen = make_plan(host, max_threads, false);
+        paths_plan_storage.upload(gen, stream);
+        if (gen.fused) {
+            paths_plan_storage.view.n = host.n;
+            paths_plan_storage.view.S = host.S;
+        }
+        paths_plan = &paths_plan_storage;
+    } else {
+        paths_plan = &fast_plan;
+    }
+
+    std::vector<uint32_t> row_of(host.nnz());
+    for (uint32_t j = 0; j < host.n; ++j)
+        for (uint32_t p = host.rowptr[j]; p < host.rowptr[j + 1]; ++p) row_of[p] = j;
+    d_gemis.upload(host.emis.data(), host.emis.size() * 4, stream);
+    d_gstart.upload(host.start.data(), host.start.size() * 4, stream);
+    d_rowptr.upload(host.rowptr.data(), host.rowptr.size() * 4, stream);
+    d_col.upload(host.col.data(), host.col.size() * 4, stream);
+    d_val.upload(host.val.data(), host.val.size() * 4, stream);
+    d_rowof.upload(row_of.data(), row_of.size() * 4, stream);
+    hip_check(hipStreamSynchronize(stream), "model upload");
+    if (kernel_pref == SVH_KERNEL_FUSED && !fast.fused)
+        throw Error(SVH_E_UNSUPPORTED, "fused kernel requested but no fused family fits this model");
+    if (!fast.fused && generic_lds_bytes(host.n) > kMaxLdsBytes)
+        throw Error(SVH_E_UNSUPPORTED, "model too large for the on-chip score vector");
+}
+
+Model::~Model() {
+    if (stream) {
+        (void)hipStreamSynchronize(stream);
+        (void)hipStreamDestroy(stream);
+    }
+}
+
+CsrModel Model::csr_view() const {
+    CsrModel c;
+    c.emis = d_gemis.as<float>();
+    c.start = d_gstart.as<float>();
+    c.rowptr = d_rowptr.as<uint32_t>();
+    c.col = d_col.as<uint32_t>();
+    c.val = d_val.as<float>();
+    c.row_of = d_rowof.as<uint32_t>();
+    c.n = host.n;
+    c.S = host.S;
+    c.nnz = host.nnz();
+    return c;
+}
+
+const DevicePlan* Model::plan_for(bool paths) const {
+    if (kernel_pref == SVH_KERNEL_GENERIC) return nullptr;
+    const DevicePlan* p = paths ? paths_plan : &fast_plan;
+    return (p && p->plan.fused) ? p : nullptr;
+}
+
+void Model::spec_build(uint32_t level, hipStream_t s) {
+    std::lock_guard<std::mutex> lock(mu);
+    DeviceGuard g(device);
+    if (!s) s = stream;
+    d_products = DeviceBuffer();
+    spec_level = 0;
+    if (level <= 1) {
+        spec_level = level;
+        return;
+    }
+    const CsrModel c = csr_view();
+    if (host.n > 65535) throw Error(SVH_E_UNSUPPORTED, "_spec level >= 2 needs states_num <= 65535");
+    pstride = (host.n + 3) & ~3u;
+    const uint64_t mat = (uint64_t)host.n * pstride;
+    uint64_t keys = host.S;
+    for (uint32_t l = 2; l <= level; ++l) {
+        keys *= host.S;
+        if (keys / host.S > 65535 / ((host.S + 31) / 32))
+            throw Error(SVH_E_UNSUPPORTED, "_spec level too high for the precompute grid");
+    }
+    const uint64_t final_bytes = keys * mat * 4;
+    const uint64_t prev_bytes = (keys / host.S) * mat * 4;
+    size_t free_b = 0, total_b = 0;
+    hip_check(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
+    if (final_bytes + prev_bytes + (64ull << 20) > free_b)
+        throw Error(SVH_E_NOMEM, "_spec products need " + std::to_string(final_bytes + prev_bytes) +
+                                     " bytes of HBM, " + std::to_string(free_b) + " free");
+    d_mfold.alloc((size_t)host.nnz() * host.S * 4);
+    hip_check(launch_spec_fold(c, d_mfold.as<float>(), s), "spec fold");
+    DeviceBuffer prev;
+    prev.alloc((size_t)host.S * mat * 4);
+    hip_check(launch_spec_densify(c, d_mfold.as<float>(), prev.as<float>(), pstride, s), "spec densify");
+    uint64_t kprev = host.S;
+    for (uint32_t l = 2; l <= level; ++l) {
+        DeviceBuffer next;
+        next.alloc((size_t)(kprev * host.S * mat * 4));
+        hip_check(launch_spec_extend(c, d_mfold.as<float>(), prev.as<float>(), kprev,
+                                     next.as<float>(), pstride, s),
+                  "spec extend");
+        hip_check(hipStreamSynchronize(s), "spec extend");
+        prev = std::move(next);
+        kprev *= host.S;
+    }
+    d_products = std::move(prev);
+    spec_level = level;
+}
+
+svh_model_info Model::info() const {
+    svh_model_info i;
+    std::memset(&i, 0, sizeof(i));
+    const DevicePlan* p = plan_for(false);
+    i.kernel = p ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
+    i.family = p ? p->plan.family : -1;
+    i.threads = p ? (int32_t)p->plan.B : (int32_t)std::min<uint32_t>(1024, round_up(host.n, 64));
+    i.slots = p ? (int32_t)p->plan.SM : 0;
+    i.light_terms = p ? (int32_t)p->plan.R : 0;
+    i.heavy_rows = p ? (int32_t)p->plan.H : 0;
+    i.heavy_uniform = (p && p->plan.mode == kHeavyUniform) ? 1 : 0;
+    i.device = device;
+    i.n = host.n;
+    i.S = host.S;
+    i.nnz = host.nnz();
+    i.lds_bytes = p ? p->plan.lds_bytes : generic_lds_bytes(host.n);
+    i.spec_level = spec_level;
+    i.spec_bytes = d_products.bytes;
+    return i;
+}
+
+// ------------------------------------------------------------------------------------------
+// Batches
+// ------------------------------------------------------------------------------------------
+Batch::Batch(Model* m, uint64_t nseq_, const uint64_t* offs, const uint64_t* symbols,
+             uint32_t flags)
+    : model(m) {
+    if (nseq_ == 0) throw Error(SVH_E_INVALID, "empty batch");
+    if (nseq_ > 0x7FFFFFFFull) throw Error(SVH_E_UNSUPPORTED, "too many sequences in one batch");
+    if (!offs || !symbols) throw Error(SVH_E_INVALID, "null offsets/symbols");
+    nseq = (uint32_t)nseq_;
+    paths = (flags & SVH_BATCH_PATHS) != 0;
+    if (paths && m->host.n >= kNoPred) throw Error(SVH_E_UNSUPPORTED, "paths need states_num < 65535");
+    offsets.assign(offs, offs + nseq + 1);
+    lens.resize(nseq);
+    std::vector<uint64_t> symoff(nseq), bpoff(nseq), pathoff(nseq);
+    uint64_t bytes = 0, bpn = 0;
+    for (uint32_t q = 0; q < nseq; ++q) {
+        if (offs[q + 1] < offs[q]) throw Error(SVH_E_INVALID, "offsets must be non-decreasing");
+        const uint64_t len = offs[q + 1] - offs[q];
+        if (len == 0)
+            throw Error(SVH_E_INVALID, "empty observation sequence (reference: seq[0] is undefined)");
+        if (len > 0xFFFFFF00ull) throw Error(SVH_E_UNSUPPORTED, "sequence too long");
+        lens[q] = (uint32_t)len;
+        symoff[q] = bytes;
+        bytes += ((len + kSymPad + 4 + 15) / 16) * 16;
+        bpoff[q] = bpn;
+        bpn += (len - 1) * (uint64_t)m->host.n;
+        pathoff[q] = offs[q] - offs[0];
+    }
+    total = offs[nseq] - offs[0];
+    std::vector<uint8_t> packed(bytes, 0);
+    const uint64_t S = m->host.S;
+    for (uint32_t q = 0; q < nseq; ++q) {
+        const uint64_t* src = symbols + offs[q];
+        uint8_t* dstp = packed.data() + symoff[q];
+        for (uint32_t i = 0; i < lens[q]; ++i) {
+            if (src[i] >= S)
+                throw Error(SVH_E_RANGE, "symbol " + std::to_string(src[i]) + " out of range (emit_num " +
+                                             std::to_string(S) + ")");
+            dstp[i] = (uint8_t)src[i];
+        }
+    }
+    DeviceGuard g(m->device);
+    hipStream_t s = m->stream;
+    d_sym.upload(packed.data(), packed.size(), s);
+    d_symoff.upload(symoff.data(), symoff.size() * 8, s);
+    std::vector<uint32_t> zeros(nseq, 0);
+    d_begin.upload(zeros.data(), zeros.size() * 4, s);
+    d_end.upload(lens.data(), lens.size() * 4, s);
+    d_scores.alloc((size_t)nseq * m->host.n * 4);
+    d_best.alloc((size_t)nseq * 8);
+    if (paths) {
+        d_bp.alloc((size_t)bpn * 2);
+        d_bpoff.upload(bpoff.data(), bpoff.size() * 8, s);
+        d_pathoff.upload(pathoff.data(), pathoff.size() * 8, s);
+        d_paths.alloc((size_t)total * 4);
+    }
+    hip_check(hipEventCreate(&ev_start), "hipEventCreate");
+    hip_check(hipEventCreate(&ev_stop), "hipEventCreate");
+    hip_check(hipStreamSynchronize(s), "batch upload");
+}
+
+Batch::~Batch() {
+    DeviceGuard g(model->device);
+    if (ev_start) (void)hipEventDestroy(ev_start);
+    if (ev_stop) (void)hipEventDestroy(ev_stop);
+}
+
+void Batch::run(uint32_t level, hipStream_t s) {
+    std::lock_guard<std::mutex> lock(model->mu);
+    DeviceGuard g(model->device);
+    if (!s) s = model->stream;
+    if (paths && level >= 2)
+        throw Error(SVH_E_UNSUPPORTED, "decoded paths are defined for the per-observation recurrence (level <= 1)");
+    if (level >= 2 && model->spec_level != level)
+        throw Error(SVH_E_STATE, "run at _spec level " + std::to_string(level) +
+                                     " needs svh_spec_build(" + std::to_string(level) + ") first");
+    const CsrModel csr = model->csr_view();
+    FusedBatch fb;
+    std::memset(&fb, 0, sizeof(fb));
+    fb.symbols = d_sym.as<uint8_t>();
+    fb.sym_off = d_symoff.as<uint64_t>();
+    fb.begin = d_begin.as<uint32_t>();
+    fb.end = d_end.as<uint32_t>();
+    fb.scores = d_scores.as<float>();
+    fb.best = d_best.as<int64_t>();
+    fb.nseq = nseq;
+    if (paths) {
+        fb.bp = d_bp.as<uint16_t>();
+        fb.bp_off = d_bpoff.as<uint64_t>();
+    }
+    auto launch_step_kernel = [&](const FusedBatch& b, bool want_paths) {
+        const DevicePlan* dp = model->plan_for(want_paths);
+        if (dp) {
+            hip_check(launch_fused(dp->view, b, dp->plan.family, want_paths, s), "fused Viterbi kernel");
+        } else {
+            const uint32_t threads = std::min<uint32_t>(1024, ((model->host.n + 63) / 64) * 64);
+            hip_check(launch_generic(csr, b, (int)threads, want_paths, s), "generic Viterbi kernel");
+        }
+    };
+
+    hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
+    if (level <= 1) {
+        launch_step_kernel(fb, paths);
+        if (paths) hip_check(launch_traceback(fb, d_pathoff.as<uint64_t>(), d_paths.as<int32_t>(),
+                                              model->host.n, s),
+                             "traceback kernel");
+    } else {
+        const uint32_t n = model->host.n;
+        if (spec_ready_level != level) {
+            std::vector<uint32_t> nch(nseq), tb(nseq), vrow(nseq);
+            for (uint32_t q = 0; q < nseq; ++q) {
+                nch[q] = (lens[q] - 1) / level;
+                tb[q] = 1 + nch[q] * level;
+                vrow[q] = (nch[q] & 1u) * nseq + q;
+            }
+            d_nchunks.upload(nch.data(), nch.size() * 4, s);
+            d_tbegin.upload(tb.data(), tb.size() * 4, s);
+            d_vrow.upload(vrow.data(), vrow.size() * 4, s);
+            d_vbuf.alloc((size_t)2 * nseq * n * 4);
+            hip_check(hipStreamSynchronize(s), "spec batch setup");
+            max_chunks = 0;
+            for (uint32_t q = 0; q < nseq; ++q) max_chunks = std::max(max_chunks, nch[q]);
+            spec_ready_level = level;
+        }
+        float* vb = d_vbuf.as<float>();
+        hip_check(launch_first_step(csr, fb.symbols, fb.sym_off, nseq, vb, s), "spec first step");
+        SpecChunkBatch cb;
+        cb.symbols = fb.symbols;
+        cb.sym_off = fb.sym_off;
+        cb.nchunks = d_nchunks.as<uint32_t>();
+        cb.nseq = nseq;
+        cb.level = level;
+        for (uint32_t c = 0; c < max_chunks; ++c) {
+            cb.chunk = c;
+            cb.v_src = vb + (size_t)(c & 1u) * nseq * n;
+            cb.v_dst = vb + (size_t)((c + 1) & 1u) * nseq * n;
+            hip_check(launch_spec_chunk(csr, model->d_products.as<float>(), cb, model->pstride, s),
+                      "spec chunk kernel");
+        }
+        FusedBatch tail = fb;
+        tail.begin = d_tbegin.as<uint32_t>();
+        tail.v_in = vb;
+        tail.v_in_row = d_vrow.as<uint32_t>();
+        tail.bp = nullptr;
+        tail.bp_off = nullptr;
+        launch_step_kernel(tail, false);
+    }
+    hip_check(hipEventRecord(ev_stop, s), "hipEventRecord");
+    ran = true;
+}
+
+void Batch::read(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out) {
+    DeviceGuard g(model->device);
+    if (!s) s = model->stream;
+    if (!ran) throw Error(SVH_E_STATE, "svh_batch_read before svh_batch_run");
+    if (paths_out && !paths) throw Error(SVH_E_STATE, "batch was created without SVH_BATCH_PATHS");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (scores)
+        hip_check(hipMemcpy(scores, d_scores.ptr, (size_t)nseq * model->host.n * 4, hipMemcpyDeviceToHost),
+                  "scores D2H");
+    if (best) hip_check(hipMemcpy(best, d_best.ptr, (size_t)nseq * 8, hipMemcpyDeviceToHost), "best D2H");
+    if (paths_out)
+        hip_check(hipMemcpy(paths_out, d_paths.ptr, (size_t)total * 4, hipMemcpyDeviceToHost), "paths D2H");
+}
+
+float Batch::elapsed_ms() {
+    DeviceGuard g(model->device);
+    if (!ran) throw Error(SVH_E_STATE, "no run recorded");
+    hip_check(hipEventSynchronize(ev_stop), "hipEventSynchronize");
+    float ms = 0;
+    hip_check(hipEventElapsedTime(&ms, ev_start, ev_stop), "hipEventElapsedTime");
+    return ms;
+}
+
+}  // namespace svh

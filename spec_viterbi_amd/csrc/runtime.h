@@ -1,0 +1,143 @@
+// Host runtime of the engine: HMM -> device model (plan + HBM upload), batches, _spec products.
+// Used by the C ABI (svh_api.cpp).  Errors are reported by throwing svh::Error.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "svh.h"
+
+namespace svh {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& msg) : std::runtime_error(msg), code(c) {}
+};
+
+void hip_check(hipError_t e, const char* what);
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev);
+    ~DeviceGuard();
+};
+
+// Device allocation owned by RAII.
+struct DeviceBuffer {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    DeviceBuffer() = default;
+    DeviceBuffer(const DeviceBuffer&) = delete;
+    DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+    DeviceBuffer(DeviceBuffer&& o) noexcept : ptr(o.ptr), bytes(o.bytes) { o.ptr = nullptr; o.bytes = 0; }
+    DeviceBuffer& operator=(DeviceBuffer&& o) noexcept;
+    ~DeviceBuffer();
+    void alloc(size_t nbytes);
+    void upload(const void* src, size_t nbytes, hipStream_t s);
+    template <class T> T* as() const { return static_cast<T*>(ptr); }
+};
+
+// Canonical host form of the model (reference semantics resolved: dense start with first
+// duplicate winning, CSR of T^T with first duplicate winning, columns ascending).
+struct HostModel {
+    uint32_t n = 0, S = 0;
+    std::vector<float> start;     // n
+    std::vector<float> emis;      // S * n
+    std::vector<uint32_t> rowptr; // n + 1
+    std::vector<uint32_t> col;    // nnz
+    std::vector<float> val;       // nnz
+    uint32_t nnz() const { return (uint32_t)col.size(); }
+};
+
+HostModel build_host_model(uint64_t n, uint64_t S, uint64_t nstart, const uint64_t* start_cols,
+                           const float* start_vals, const float* emissions, uint64_t ntrans,
+                           const uint64_t* src, const uint64_t* dst, const float* prob);
+
+// Register/LDS schedule of the fused kernel.
+struct Plan {
+    bool fused = false;
+    int family = -1;
+    uint32_t B = 0, SM = 0, R = 0, HM = 0, XM = 0, H = 0;
+    int mode = kHeavyGeneral;
+    uint32_t estride = 0, vstride = 0;
+    int hrow[kMaxHeavy] = {0, 0, 0, 0};
+    float hw[kMaxHeavy] = {0, 0, 0, 0};
+    uint32_t xk[kMaxHeavy][kMaxExc] = {};
+    float xw[kMaxHeavy][kMaxExc] = {};
+    std::vector<uint32_t> lcol;
+    std::vector<float> lval;
+    std::vector<float> hval;
+    std::vector<uint8_t> hvalid;
+    std::vector<float> hmask;
+    std::vector<float> emis_pad;   // S * estride (+ tail)
+    std::vector<float> start_pad;  // estride + 16
+    size_t lds_bytes = 0;
+};
+
+// Build the fused plan, or return plan.fused == false when no family fits.  allow_uniform=false
+// restricts to term-by-term heavy rows (needed for argmin backpointers).
+Plan make_plan(const HostModel& hm, int max_threads, bool allow_uniform);
+
+// A plan resident in HBM plus the kernel-argument view of it.
+struct DevicePlan {
+    Plan plan;
+    DeviceBuffer d_emis, d_start, d_lcol, d_lval, d_hval, d_hvalid, d_hmask;
+    FusedModel view{};
+    void upload(const Plan& p, hipStream_t s);
+};
+
+struct Model {
+    std::mutex mu;
+    int device = 0;
+    int kernel_pref = SVH_KERNEL_AUTO;
+    HostModel host;
+    hipStream_t stream = nullptr;
+    DevicePlan fast_plan;            // fastest fused plan (may use uniform heavy rows)
+    DevicePlan paths_plan_storage;   // term-by-term plan when fast_plan is uniform
+    const DevicePlan* paths_plan = nullptr;
+    DeviceBuffer d_gemis, d_gstart, d_rowptr, d_col, d_val, d_rowof;  // CSR (generic, _spec)
+    // _spec products
+    uint32_t spec_level = 0;
+    uint32_t pstride = 0;
+    DeviceBuffer d_mfold, d_products;
+
+    Model(const HostModel& h, const svh_model_opts* opts);
+    ~Model();
+    CsrModel csr_view() const;
+    // Fused plan to run (nullptr: generic kernel).
+    const DevicePlan* plan_for(bool paths) const;
+    void spec_build(uint32_t level, hipStream_t s);
+    svh_model_info info() const;
+};
+
+struct Batch {
+    Model* model;
+    uint32_t nseq = 0;
+    bool paths = false;
+    std::vector<uint64_t> offsets;  // host copy of the caller's prefix offsets
+    std::vector<uint32_t> lens;
+    uint64_t total = 0;
+    DeviceBuffer d_sym, d_symoff, d_begin, d_end, d_scores, d_best;
+    DeviceBuffer d_bp, d_bpoff, d_pathoff, d_paths;
+    // _spec runs
+    DeviceBuffer d_vbuf, d_nchunks, d_tbegin, d_vrow;
+    uint32_t spec_ready_level = 0;
+    uint32_t max_chunks = 0;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    bool ran = false;
+
+    Batch(Model* m, uint64_t nseq, const uint64_t* offsets, const uint64_t* symbols, uint32_t flags);
+    ~Batch();
+    void run(uint32_t level, hipStream_t s);
+    void read(hipStream_t s, float* scores, int64_t* best, int32_t* paths);
+    float elapsed_ms();
+};
+
+}  // namespace svh

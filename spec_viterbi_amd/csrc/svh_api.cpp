@@ -1,0 +1,247 @@
+// extern "C" boundary (include/svh.h).  Every entry point catches everything, records a
+// thread-local message and returns a status code: no exception crosses the ABI.
+#include <fstream>
+#include <memory>
+#include <new>
+#include <string>
+
+#include "HMM.h"
+#include "data_reader.h"
+#include "runtime.h"
+#include "svh.h"
+
+struct svh_hmm {
+    HMM hmm;
+};
+struct svh_ess {
+    HMM::Emit_seq_vec_t seqs;
+};
+struct svh_model {
+    std::unique_ptr<svh::Model> impl;
+};
+struct svh_batch {
+    std::unique_ptr<svh::Batch> impl;
+    svh_model* owner;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        g_last_error.clear();
+        f();
+        return SVH_OK;
+    } catch (const svh::Error& e) {
+        return fail(e.code, e.what());
+    } catch (const std::bad_alloc&) {
+        return fail(SVH_E_NOMEM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(SVH_E_INVALID, e.what());
+    } catch (...) {
+        return fail(SVH_E_INVALID, "unknown error");
+    }
+}
+
+void require(bool ok, const char* what) {
+    if (!ok) throw svh::Error(SVH_E_INVALID, what);
+}
+
+}  // namespace
+
+extern "C" {
+
+int svh_abi_version(void) { return SVH_ABI_VERSION; }
+
+const char* svh_last_error(void) { return g_last_error.c_str(); }
+
+int svh_device_count(int* count) {
+    return guarded([&] {
+        require(count != nullptr, "null count");
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+        *count = c;
+    });
+}
+
+// ---- readers -------------------------------------------------------------------------------
+int svh_hmm_read(const char* path, svh_hmm_t* out) {
+    return guarded([&] {
+        require(path && out, "null argument");
+        *out = nullptr;
+        if (!std::ifstream(path)) throw svh::Error(SVH_E_IO, std::string("cannot open ") + path);
+        auto h = std::make_unique<svh_hmm>();
+        h->hmm = read_HMM(path);
+        *out = h.release();
+    });
+}
+
+int svh_hmm_dims(svh_hmm_t h, uint64_t* n, uint64_t* S, uint64_t* nstart, uint64_t* ntrans) {
+    return guarded([&] {
+        require(h != nullptr, "null handle");
+        if (n) *n = h->hmm.states_num;
+        if (S) *S = h->hmm.emit_num;
+        if (nstart) *nstart = h->hmm.start_probabilities.size();
+        if (ntrans) *ntrans = h->hmm.trans_probs.size();
+    });
+}
+
+int svh_hmm_copy(svh_hmm_t h, uint64_t* start_cols, float* start_vals, float* emissions,
+                 uint64_t* trans_src, uint64_t* trans_dst, float* trans_prob) {
+    return guarded([&] {
+        require(h != nullptr, "null handle");
+        const HMM& m = h->hmm;
+        for (size_t i = 0; i < m.start_probabilities.size(); ++i) {
+            if (start_cols) start_cols[i] = m.start_probabilities_cols[i];
+            if (start_vals) start_vals[i] = m.start_probabilities[i];
+        }
+        if (emissions)
+            for (size_t o = 0; o < m.emissions.size(); ++o)
+                for (size_t j = 0; j < m.emissions[o].size(); ++j)
+                    emissions[o * m.states_num + j] = m.emissions[o][j];
+        for (size_t e = 0; e < m.trans_probs.size(); ++e) {
+            if (trans_src) trans_src[e] = m.trans_rows[e];
+            if (trans_dst) trans_dst[e] = m.trans_cols[e];
+            if (trans_prob) trans_prob[e] = m.trans_probs[e];
+        }
+    });
+}
+
+void svh_hmm_free(svh_hmm_t h) { delete h; }
+
+int svh_ess_read(const char* path, svh_ess_t* out) {
+    return guarded([&] {
+        require(path && out, "null argument");
+        *out = nullptr;
+        if (!std::ifstream(path)) throw svh::Error(SVH_E_IO, std::string("cannot open ") + path);
+        auto e = std::make_unique<svh_ess>();
+        e->seqs = read_emit_seq(path);
+        *out = e.release();
+    });
+}
+
+int svh_ess_dims(svh_ess_t e, uint64_t* nseq, uint64_t* total) {
+    return guarded([&] {
+        require(e != nullptr, "null handle");
+        uint64_t t = 0;
+        for (const auto& s : e->seqs) t += s.size();
+        if (nseq) *nseq = e->seqs.size();
+        if (total) *total = t;
+    });
+}
+
+int svh_ess_copy(svh_ess_t e, uint64_t* offsets, uint64_t* symbols) {
+    return guarded([&] {
+        require(e != nullptr, "null handle");
+        uint64_t t = 0;
+        for (size_t q = 0; q < e->seqs.size(); ++q) {
+            if (offsets) offsets[q] = t;
+            for (size_t i = 0; i < e->seqs[q].size(); ++i)
+                if (symbols) symbols[t + i] = e->seqs[q][i];
+            t += e->seqs[q].size();
+        }
+        if (offsets) offsets[e->seqs.size()] = t;
+    });
+}
+
+void svh_ess_free(svh_ess_t e) { delete e; }
+
+// ---- model ---------------------------------------------------------------------------------
+int svh_model_create(uint64_t n, uint64_t S, uint64_t nstart, const uint64_t* start_cols,
+                     const float* start_vals, const float* emissions, uint64_t ntrans,
+                     const uint64_t* trans_src, const uint64_t* trans_dst,
+                     const float* trans_prob, const svh_model_opts* opts, svh_model_t* out) {
+    return guarded([&] {
+        require(out != nullptr, "null output handle");
+        *out = nullptr;
+        svh::HostModel h = svh::build_host_model(n, S, nstart, start_cols, start_vals, emissions,
+                                                 ntrans, trans_src, trans_dst, trans_prob);
+        auto m = std::make_unique<svh_model>();
+        m->impl = std::make_unique<svh::Model>(h, opts);
+        *out = m.release();
+    });
+}
+
+int svh_model_destroy(svh_model_t m) {
+    return guarded([&] { delete m; });
+}
+
+int svh_model_get_info(svh_model_t m, svh_model_info* info) {
+    return guarded([&] {
+        require(m && info, "null argument");
+        *info = m->impl->info();
+    });
+}
+
+int svh_spec_build(svh_model_t m, uint32_t level, void* stream) {
+    return guarded([&] {
+        require(m != nullptr, "null model");
+        m->impl->spec_build(level, static_cast<hipStream_t>(stream));
+    });
+}
+
+// ---- batches -------------------------------------------------------------------------------
+int svh_batch_create(svh_model_t m, uint64_t nseq, const uint64_t* offsets,
+                     const uint64_t* symbols, uint32_t flags, svh_batch_t* out) {
+    return guarded([&] {
+        require(m && out, "null argument");
+        *out = nullptr;
+        auto b = std::make_unique<svh_batch>();
+        b->owner = m;
+        b->impl = std::make_unique<svh::Batch>(m->impl.get(), nseq, offsets, symbols, flags);
+        *out = b.release();
+    });
+}
+
+int svh_batch_run(svh_batch_t b, uint32_t level, void* stream) {
+    return guarded([&] {
+        require(b != nullptr, "null batch");
+        b->impl->run(level, static_cast<hipStream_t>(stream));
+    });
+}
+
+int svh_batch_read(svh_batch_t b, void* stream, float* scores, int64_t* best_state,
+                   int32_t* paths) {
+    return guarded([&] {
+        require(b != nullptr, "null batch");
+        b->impl->read(static_cast<hipStream_t>(stream), scores, best_state, paths);
+    });
+}
+
+int svh_batch_device_results(svh_batch_t b, float** scores, int64_t** best_state) {
+    return guarded([&] {
+        require(b != nullptr, "null batch");
+        if (scores) *scores = b->impl->d_scores.as<float>();
+        if (best_state) *best_state = b->impl->d_best.as<int64_t>();
+    });
+}
+
+int svh_batch_elapsed_ms(svh_batch_t b, float* ms) {
+    return guarded([&] {
+        require(b && ms, "null argument");
+        *ms = b->impl->elapsed_ms();
+    });
+}
+
+int svh_batch_destroy(svh_batch_t b) {
+    return guarded([&] { delete b; });
+}
+
+int svh_viterbi(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* offsets,
+                const uint64_t* symbols, float* scores, int64_t* best_state, int32_t* paths) {
+    return guarded([&] {
+        require(m != nullptr, "null model");
+        svh::Batch b(m->impl.get(), nseq, offsets, symbols, paths ? SVH_BATCH_PATHS : 0u);
+        b.run(level, nullptr);
+        b.read(nullptr, scores, best_state, paths);
+    });
+}
+
+}  // extern "C"

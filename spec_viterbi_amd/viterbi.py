@@ -1,0 +1,205 @@
+"""Reference-interface backends on the HIP engine.
+
+`Viterbi_impl` / `Viterbi_spec_impl` mirror the reference's abstract classes
+(Viterbi_impl/Viterbi_impl.h:6-11, Viterbi_spec_impl.h:6-24); `HIP_impl` / `HIP_spec_impl` are
+the MI355X backends (same names as the C++ classes in include/HIP_impl.h, HIP_spec_impl.h).
+`DeviceModel` / `DeviceBatch` expose the batched, HBM-resident API underneath (include/svh.h).
+"""
+from __future__ import annotations
+
+import abc
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .hmm import HMM, pack_sequences
+
+_u64 = ctypes.POINTER(ctypes.c_uint64)
+_f32 = ctypes.POINTER(ctypes.c_float)
+_i64 = ctypes.POINTER(ctypes.c_int64)
+_i32 = ctypes.POINTER(ctypes.c_int32)
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+class DeviceModel:
+    """An HMM resident in HBM on one device (svh_model_create)."""
+
+    def __init__(self, hmm: HMM, device: int = -1, kernel: int = _lib.SVH_KERNEL_AUTO, max_threads: int = 0):
+        self.n = int(hmm.states_num)
+        self.S = int(hmm.emit_num)
+        opts = _lib.svh_model_opts(device, kernel, max_threads, 0)
+        h = ctypes.c_void_p()
+        sc = np.ascontiguousarray(hmm.start_probabilities_cols, np.uint64)
+        sv = np.ascontiguousarray(hmm.start_probabilities, np.float32)
+        em = np.ascontiguousarray(hmm.emissions, np.float32)
+        src = np.ascontiguousarray(hmm.trans_rows, np.uint64)
+        dst = np.ascontiguousarray(hmm.trans_cols, np.uint64)
+        pr = np.ascontiguousarray(hmm.trans_probs, np.float32)
+        _lib.check(_lib.lib.svh_model_create(self.n, self.S, sc.size, _p(sc, _u64), _p(sv, _f32), _p(em, _f32),
+                                             pr.size, _p(src, _u64), _p(dst, _u64), _p(pr, _f32),
+                                             ctypes.byref(opts), ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self) -> dict:
+        i = _lib.svh_model_info()
+        _lib.check(_lib.lib.svh_model_get_info(self._h, ctypes.byref(i)))
+        return {name: getattr(i, name) for name, _ in i._fields_}
+
+    def spec_build(self, level: int, stream: int | None = None) -> None:
+        _lib.check(_lib.lib.svh_spec_build(self._h, int(level), ctypes.c_void_p(stream or 0)))
+
+    def batch(self, seqs, paths: bool = False) -> "DeviceBatch":
+        return DeviceBatch(self, seqs, paths)
+
+    def viterbi(self, seqs, level: int = 0, paths: bool = False):
+        """One-shot: scores [nseq, n] (+ best state [nseq], + paths list if requested)."""
+        offsets, symbols = pack_sequences(seqs)
+        nseq = offsets.size - 1
+        scores = np.empty((nseq, self.n), np.float32)
+        best = np.empty(nseq, np.int64)
+        pth = np.empty(int(offsets[-1]), np.int32) if paths else None
+        _lib.check(_lib.lib.svh_viterbi(self._h, int(level), nseq, _p(offsets, _u64), _p(symbols, _u64),
+                                        _p(scores, _f32), _p(best, _i64),
+                                        _p(pth, _i32) if paths else None))
+        if paths:
+            return scores, best, [pth[offsets[q]:offsets[q + 1]] for q in range(nseq)]
+        return scores, best
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib.svh_model_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceBatch:
+    """Sequences resident in HBM; run() enqueues one pass on a HIP stream (svh_batch_*)."""
+
+    def __init__(self, model: DeviceModel, seqs, paths: bool = False):
+        self.model = model
+        self.offsets, symbols = pack_sequences(seqs)
+        self.nseq = self.offsets.size - 1
+        self.paths = paths
+        self.total = int(self.offsets[-1])
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib.svh_batch_create(model.handle, self.nseq, _p(self.offsets, _u64), _p(symbols, _u64),
+                                             _lib.SVH_BATCH_PATHS if paths else 0, ctypes.byref(h)))
+        self._h = h
+
+    def run(self, level: int = 0, stream: int | None = None) -> None:
+        _lib.check(_lib.lib.svh_batch_run(self._h, int(level), ctypes.c_void_p(stream or 0)))
+
+    def read(self, stream: int | None = None, want_paths: bool = False):
+        scores = np.empty((self.nseq, self.model.n), np.float32)
+        best = np.empty(self.nseq, np.int64)
+        pth = np.empty(self.total, np.int32) if want_paths else None
+        _lib.check(_lib.lib.svh_batch_read(self._h, ctypes.c_void_p(stream or 0), _p(scores, _f32), _p(best, _i64),
+                                           _p(pth, _i32) if want_paths else None))
+        if want_paths:
+            return scores, best, [pth[self.offsets[q]:self.offsets[q + 1]] for q in range(self.nseq)]
+        return scores, best
+
+    def device_results(self) -> tuple[int, int]:
+        s, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(_lib.lib.svh_batch_device_results(self._h, ctypes.byref(s), ctypes.byref(b)))
+        return int(s.value or 0), int(b.value or 0)
+
+    def elapsed_ms(self) -> float:
+        ms = ctypes.c_float()
+        _lib.check(_lib.lib.svh_batch_elapsed_ms(self._h, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib.svh_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Viterbi_impl(abc.ABC):
+    """Reference: Viterbi_impl/Viterbi_impl.h:6-11."""
+
+    @abc.abstractmethod
+    def run_Viterbi(self, hmm: HMM, seq) -> np.ndarray:
+        ...
+
+
+class Viterbi_spec_impl(abc.ABC):
+    """Reference: Viterbi_impl/Viterbi_spec_impl.h:6-24."""
+
+    def __init__(self, level: int):
+        self.level = int(level)
+
+    @abc.abstractmethod
+    def spec_with(self, hmm: HMM) -> None:
+        ...
+
+    @abc.abstractmethod
+    def run_Viterbi_spec(self, seq) -> np.ndarray:
+        ...
+
+    def get_level(self) -> int:
+        return self.level
+
+
+class HIP_impl(Viterbi_impl):
+    """MI355X backend of Viterbi_impl; the device model is cached per HMM object."""
+
+    def __init__(self, device: int = -1, **model_opts):
+        self.device = device
+        self.model_opts = model_opts
+        self._cache: tuple[int, DeviceModel] | None = None
+
+    def _model(self, hmm: HMM) -> DeviceModel:
+        if self._cache is None or self._cache[0] != id(hmm):
+            self._cache = (id(hmm), DeviceModel(hmm, self.device, **self.model_opts))
+        return self._cache[1]
+
+    def run_Viterbi(self, hmm: HMM, seq) -> np.ndarray:
+        return self._model(hmm).viterbi([seq])[0][0]
+
+    def run_Viterbi_batch(self, hmm: HMM, seqs) -> np.ndarray:
+        return self._model(hmm).viterbi(seqs)[0]
+
+    def decode_path(self, hmm: HMM, seq) -> np.ndarray:
+        return self._model(hmm).viterbi([seq], paths=True)[2][0]
+
+
+class HIP_spec_impl(Viterbi_spec_impl):
+    """MI355X backend of Viterbi_spec_impl (level >= 2: products precomputed in HBM)."""
+
+    def __init__(self, level: int, device: int = -1, **model_opts):
+        super().__init__(level)
+        self.device = device
+        self.model_opts = model_opts
+        self._model: DeviceModel | None = None
+
+    def spec_with(self, hmm: HMM) -> None:
+        self._model = DeviceModel(hmm, self.device, **self.model_opts)
+        self._model.spec_build(self.level)
+
+    def run_Viterbi_spec(self, seq) -> np.ndarray:
+        return self.run_Viterbi_spec_batch([seq])[0]
+
+    def run_Viterbi_spec_batch(self, seqs) -> np.ndarray:
+        if self._model is None:
+            raise RuntimeError("run_Viterbi_spec before spec_with")
+        return self._model.viterbi(seqs, level=self.level)[0]

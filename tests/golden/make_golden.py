@@ -1,0 +1,65 @@
+"""Generate the committed golden vectors (tests/golden/*.json) from the CPU oracle.
+
+The oracle (oracle/viterbi_oracle.c) restates GraphBLAS_impl / GraphBLAS_spec_impl and is pinned
+by the reference's own fixtures (tests/test_helper.h:17-22) -- see tests/test_oracle_golden.py.
+Floats are stored as IEEE-754 bit patterns (hex) so the vectors are exact.
+
+    python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import struct
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+import spec_viterbi_amd as svh  # noqa: E402  (native reader only; no GPU needed)
+from oracle import oracle  # noqa: E402
+
+DATA = os.path.join(ROOT, "data")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def hexbits(a) -> list[str]:
+    return [struct.pack("<f", float(x)).hex() for x in np.asarray(a, np.float32).ravel()]
+
+
+def case(hmm_path, ess_path, seq_ids, levels=(), paths=True):
+    hmm = svh.read_HMM(os.path.join(DATA, hmm_path))
+    seqs = svh.read_emit_seq(os.path.join(DATA, ess_path))
+    out = {"chmm": hmm_path, "ess": ess_path, "sequences": []}
+    for q in seq_ids:
+        seq = seqs[q]
+        rec = {"index": q, "length": int(seq.size)}
+        if paths:
+            scores, best, path = oracle.decode(hmm, seq)
+            rec["best_state"] = best
+            rec["path"] = path.tolist()
+        else:
+            scores = oracle.viterbi(hmm, seq)
+        rec["scores"] = hexbits(scores)
+        rec["spec"] = {str(L): hexbits(oracle.viterbi_spec(hmm, L, seq)) for L in levels}
+        out["sequences"].append(rec)
+    return out
+
+
+def main():
+    goldens = {
+        "test_chmms": [case(f"chmm_files/test_chmms/{i}_test_chmm.chmm", f"ess_files/test_sequences/{i}_test_seq.ess",
+                            range(2 if i == 0 else 1), levels=(1, 2, 3)) for i in range(4)],
+        "chmm100_emit3": case("chmm_files/100.chmm", "ess_files/emit_3_3500_20.ess", range(3), levels=(2,)),
+        "chmm2405_emit50": case("chmm_files/2405.chmm", "ess_files/emit_50_3500_20.ess", range(2)),
+    }
+    for name, val in goldens.items():
+        with open(os.path.join(OUT, f"{name}.json"), "w") as f:
+            json.dump(val, f, separators=(",", ":"))
+        print("wrote", name)
+
+
+if __name__ == "__main__":
+    main()

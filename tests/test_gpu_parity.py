@@ -1,0 +1,175 @@
+"""GPU parity: the HIP path (through the C ABI) vs the oracle / committed goldens, bit-exact.
+
+Scores must be bit-identical to GraphBLAS_impl's association (-0.0 == +0.0), best states and
+decoded paths identical (lowest index on ties).
+"""
+import numpy as np
+import pytest
+
+import spec_viterbi_amd as svh
+from spec_viterbi_amd import _lib
+from oracle import oracle
+from tests.conftest import chmm, ess
+from tests.helpers import bit_equal, first_mismatch, from_hex, load_golden, random_hmm, random_seqs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    assert _lib.device_count() > 0, "no HIP device visible (GPU tests must run on an MI355X)"
+
+
+def check_against_oracle(hmm, seqs, kernel=_lib.SVH_KERNEL_AUTO, max_threads=0, paths=True):
+    model = svh.DeviceModel(hmm, kernel=kernel, max_threads=max_threads)
+    if paths:
+        scores, best, pth = model.viterbi(seqs, paths=True)
+    else:
+        scores, best = model.viterbi(seqs)
+    for q, seq in enumerate(seqs):
+        if paths:
+            ref, ref_best, ref_path = oracle.decode(hmm, seq)
+        else:
+            ref = oracle.viterbi(hmm, seq)
+            ref_best = int(np.argmin(ref)) if np.isfinite(ref).any() else 0
+        assert bit_equal(scores[q], ref), (q, first_mismatch(scores[q], ref), model.info())
+        assert best[q] == ref_best, (q, best[q], ref_best)
+        if paths:
+            assert np.array_equal(pth[q], ref_path), (q, np.nonzero(pth[q] != ref_path)[0][:5])
+    return model
+
+
+@pytest.mark.parametrize("i", range(4))
+def test_reference_fixtures(i):
+    hmm = svh.read_HMM(chmm(f"test_chmms/{i}_test_chmm.chmm"))
+    seqs = svh.read_emit_seq(ess(f"test_sequences/{i}_test_seq.ess"))
+    check_against_oracle(hmm, seqs)
+    check_against_oracle(hmm, seqs, kernel=_lib.SVH_KERNEL_GENERIC)
+
+
+def test_cpp_interface_fixtures_through_python_mirror():
+    impl = svh.HIP_impl()
+    expected = load_golden("test_chmms")
+    for i, case in enumerate(expected):
+        hmm = svh.read_HMM(chmm(f"test_chmms/{i}_test_chmm.chmm"))
+        seqs = svh.read_emit_seq(ess(f"test_sequences/{i}_test_seq.ess"))
+        for rec in case["sequences"]:
+            assert bit_equal(impl.run_Viterbi(hmm, seqs[rec["index"]]), from_hex(rec["scores"]))
+            assert list(impl.decode_path(hmm, seqs[rec["index"]])) == rec["path"]
+
+
+@pytest.mark.parametrize("name", ["chmm100_emit3", "chmm2405_emit50"])
+def test_committed_goldens(name):
+    g = load_golden(name)
+    hmm = svh.read_HMM(chmm(g["chmm"].split("chmm_files/")[1]))
+    seqs = svh.read_emit_seq(ess(g["ess"].split("ess_files/")[1]))
+    idx = [r["index"] for r in g["sequences"]]
+    model = svh.DeviceModel(hmm)
+    scores, best, pth = model.viterbi([seqs[i] for i in idx], paths=True)
+    for k, rec in enumerate(g["sequences"]):
+        assert bit_equal(scores[k], from_hex(rec["scores"])), first_mismatch(scores[k], from_hex(rec["scores"]))
+        assert best[k] == rec["best_state"]
+        assert pth[k].tolist() == rec["path"]
+
+
+def test_2405_emit50_full_batch_vs_oracle():
+    """configs[2]: 2405.chmm x emit_50_3500_20 (all 50 sequences), non-spec path."""
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
+    model = svh.DeviceModel(hmm)
+    info = model.info()
+    assert info["kernel"] == _lib.SVH_KERNEL_FUSED and info["heavy_uniform"] == 1, info
+    scores, best = model.viterbi(seqs)
+    ref, _ = oracle.viterbi_batch(hmm, seqs, nthreads=16)
+    for q in range(len(seqs)):
+        assert bit_equal(scores[q], ref[q]), (q, first_mismatch(scores[q], ref[q]))
+        assert best[q] == int(np.argmin(ref[q]))
+
+
+@pytest.mark.parametrize("name", ["100.chmm", "200.chmm", "500.chmm", "1001.chmm", "1509.chmm", "2050.chmm",
+                                  "2365.chmm"])
+def test_pfam_models_emit3(name):
+    hmm = svh.read_HMM(chmm(name))
+    seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    check_against_oracle(hmm, seqs[:2], paths=False)
+
+
+def test_covid_ragged_batch():
+    """configs[4] data: 16 sequences of lengths 38..7096 (> the 4096-symbol LDS ring)."""
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("covid-19.ess"))
+    check_against_oracle(hmm, seqs, paths=False)
+
+
+def test_paths_on_large_model():
+    hmm = svh.read_HMM(chmm("900.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    check_against_oracle(hmm, seqs[:1], paths=True)
+
+
+@pytest.mark.parametrize("threads", [64, 128, 256, 512])
+def test_workgroup_geometries(threads):
+    hmm = svh.read_HMM(chmm("300.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    check_against_oracle(hmm, [s[:700] for s in seqs], max_threads=threads)
+
+
+@pytest.mark.parametrize("n,degree,dense,seed", [
+    (900, 3, (), 1),          # chmm_gen.py shape: in-degree ~Poisson(3) -> R4/R8/R16 families
+    (257, 2, (5,), 2),        # one dense row -> general heavy rows
+    (300, 3, (0, 7, 299), 3),  # three dense rows -> R4+ families
+    (64, 1, (), 4),
+    (1, 1, (), 5),            # single state
+])
+def test_random_models(n, degree, dense, seed):
+    hmm = random_hmm(n, out_degree=degree, dense_rows=dense, seed=seed, zero_emis=0.05)
+    seqs = random_seqs(20, [1, 2, 3, 17, 500], seed=seed)
+    check_against_oracle(hmm, seqs)
+    check_against_oracle(hmm, seqs, kernel=_lib.SVH_KERNEL_GENERIC)
+
+
+def test_high_indegree_falls_back_to_generic():
+    hmm = random_hmm(200, out_degree=30, seed=9)  # in-degree ~30: no fused family fits
+    model = check_against_oracle(hmm, random_seqs(20, [50, 300], seed=9))
+    assert model.info()["kernel"] == _lib.SVH_KERNEL_GENERIC
+
+
+def test_duplicate_transitions_first_wins():
+    base = svh.read_HMM(chmm("test_chmms/3_test_chmm.chmm"))
+    # duplicate (1 -> 2) with a different probability appended: GrB_FIRST keeps the original
+    hmm = svh.HMM(states_num=base.states_num, emit_num=base.emit_num, trans_num=base.trans_num + 1,
+                  trans_rows=np.append(base.trans_rows, 1), trans_cols=np.append(base.trans_cols, 2),
+                  trans_probs=np.append(base.trans_probs, np.float32(0.01)), emissions=base.emissions,
+                  start_probabilities_cols=np.append(base.start_probabilities_cols, 0),
+                  start_probabilities=np.append(base.start_probabilities, np.float32(5.0)))
+    seqs = svh.read_emit_seq(ess("test_sequences/3_test_seq.ess"))
+    check_against_oracle(hmm, seqs)
+
+
+def test_errors():
+    hmm = svh.read_HMM(chmm("test_chmms/0_test_chmm.chmm"))
+    model = svh.DeviceModel(hmm)
+    with pytest.raises(_lib.SvhError) as e:
+        model.viterbi([np.array([0, 4], np.uint64)])  # symbol 4 >= emit_num 4
+    assert e.value.code == _lib.SVH_E_RANGE
+    with pytest.raises(_lib.SvhError) as e:
+        model.viterbi([np.array([], np.uint64)])
+    assert e.value.code == _lib.SVH_E_INVALID
+    with pytest.raises(_lib.SvhError) as e:
+        model.viterbi([np.array([0, 1], np.uint64)], level=2)  # spec products not built
+    assert e.value.code == _lib.SVH_E_STATE
+
+
+def test_batch_api_device_resident_rerun():
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))[:4]
+    model = svh.DeviceModel(hmm)
+    batch = model.batch(seqs)
+    batch.run()
+    a, _ = batch.read()
+    batch.run()
+    b, _ = batch.read()
+    assert bit_equal(a, b)
+    assert batch.elapsed_ms() > 0
+    ref, _ = oracle.viterbi_batch(hmm, seqs)
+    assert bit_equal(a, ref)
