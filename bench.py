@@ -106,8 +106,12 @@ def main():
     if args.level >= 2:
         model.spec_build(args.level)
     batch = model.batch(seqs)
-    stream = torch.cuda.current_stream()
+    # A stream of our own: torch's default stream has handle 0, which the C ABI reads as "the
+    # model's own stream", so events recorded on torch's default stream would not bracket the
+    # kernel.  Every launch and every event below goes to this one stream.
+    stream = torch.cuda.Stream(device=local)
     sptr = stream.cuda_stream
+    assert sptr, "expected a non-null HIP stream handle"
 
     for _ in range(args.warmup):
         batch.run(args.level, sptr)

@@ -50,6 +50,7 @@ def random_hmm(n, S=20, out_degree=3, nstart=2, seed=0, dense_rows=(), self_loop
     from spec_viterbi_amd import HMM
 
     rng = np.random.default_rng(seed)
+    nstart = min(nstart, n)
 
     def probs(k):
         w = rng.integers(1, 100, size=k).astype(np.float64)
