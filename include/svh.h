@@ -64,12 +64,18 @@ int svh_ess_copy(svh_ess_t e, uint64_t* offsets /* nseq + 1 */, uint64_t* symbol
 void svh_ess_free(svh_ess_t e);
 
 /* ---- model: HMM resident in HBM -------------------------------------------------------- */
-enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2 };
+/* AUTO: for scores-only passes over chain-shaped (MSV) models the barrier-free register chain
+ * kernel (CHAIN, emit_num <= 32, <= 2560 light states), else the barrier chain kernel (BAND);
+ * otherwise the fused kernel, else the generic one.  BAND / CHAIN force that kernel (error if the
+ * model does not qualify); path runs always use the fused (or generic) kernel. */
+enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2, SVH_KERNEL_BAND = 3,
+       SVH_KERNEL_CHAIN = 4 };
 
 typedef struct {
     int32_t device;      /* HIP device ordinal; -1 = the caller's current device */
     int32_t kernel;      /* SVH_KERNEL_* */
-    int32_t max_threads; /* fused-kernel workgroup size cap (64..512, multiple of 64); 0 = 512 */
+    int32_t max_threads; /* workgroup size cap (multiple of 64, <= 1024; the fused kernel caps at
+                            512); 0 = each kernel's default */
     int32_t reserved;
 } svh_model_opts;
 
@@ -83,7 +89,7 @@ int svh_model_create(uint64_t n, uint64_t S, uint64_t nstart, const uint64_t* st
 int svh_model_destroy(svh_model_t m);
 
 typedef struct {
-    int32_t kernel;        /* SVH_KERNEL_FUSED or SVH_KERNEL_GENERIC (what runs) */
+    int32_t kernel;        /* SVH_KERNEL_CHAIN, _BAND, _FUSED or _GENERIC (scores-only runs) */
     int32_t family;        /* fused family id (0: R2 uniform-heavy, 1: R2, 2: R4, 3: R8, 4: R16) */
     int32_t threads;       /* workgroup size */
     int32_t slots;         /* states per thread */

@@ -24,6 +24,8 @@ SVH_E_IO = -7
 SVH_KERNEL_AUTO = 0
 SVH_KERNEL_FUSED = 1
 SVH_KERNEL_GENERIC = 2
+SVH_KERNEL_BAND = 3
+SVH_KERNEL_CHAIN = 4
 SVH_BATCH_PATHS = 1
 
 

@@ -1,0 +1,425 @@
+// Barrier-free chain Viterbi kernel (gfx950) for MSV-shaped models (N, M_1..M_L, C; the shape of
+// every reference .chmm, chmm_files/silent_hmm_to_chmm.py), emit_num <= 32.
+//
+// Reference hot loop: Viterbi_impl/GraphBLAS_impl.cpp:59-73 (same association, bit-identical):
+//     v'[j] = min_k fl( fl(E[o][j] + T^T[j][k]) + v[k] )
+//
+// One workgroup per sequence; its waves never meet at an s_barrier inside the loop.
+//   * Light scores, the weights of their two terms and the emission table of the thread's own
+//     positions for every symbol live in VGPRs (E[o] is picked by the wave-uniform symbol with
+//     s_set_gpr_idx), so the loop issues no LDS traffic for them and no vector-memory traffic
+//     except one symbol word every four observations.
+//   * Position p = t*SM + s is slot s of thread t: the chain predecessor of slot 0 is lane-1's
+//     last slot (DPP wave_shr:1); lane 0 takes the previous wave's last value of the previous
+//     observation from a tagged LDS word (value | observation tag, one 64-bit word).
+//   * Heavy rows: min_{k in U} fl(a + v[k]) == fl(a + min_{k in U} v[k]) (fp32 add is monotone),
+//     U = all light rows.  Each wave publishes its partial min of every observation as a tagged
+//     word; the heavy scores of observation i-1 are computed (redundantly, in every thread) at
+//     observation i from the partials of i-2, so the all-wave exchange has one observation of
+//     slack and the waves drift freely by up to two observations.
+//   * Rings of 4 tagged words per wave make overwrites safe: a wave at observation i has seen
+//     every wave finish observation i-2.  Every spin is bounded (fault word on give-up).
+#include "device_common.h"
+#include "kernels.h"
+
+namespace svh {
+
+using namespace dev;
+
+namespace {
+
+typedef float f32x32 __attribute__((ext_vector_type(32)));
+
+constexpr uint32_t kRing = 4;  // see the ring argument in the step comments
+constexpr uint32_t kSpinLimit = 1u << 22;
+
+// Empty asm that consumes the values: everything computing them is emitted before it.
+template <int N>
+__device__ __forceinline__ void pin(float (&x)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) asm volatile("" : "+v"(x[k]));
+}
+
+__device__ __forceinline__ float wave_shr1(float x, float old) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                                  __builtin_bit_cast(int, x), 0x138,
+                                                                  0xf, 0xf, false));
+}
+
+
+// Every wave publishes, for observation k, two tagged 8-byte words: {partial of k-1, k+1} in
+// part[k % kRing][wave] and {boundary of k, k+1} in bnd[k % kRing][wave] (tag 0 = never written).
+// Polls read them with relaxed 64-bit atomic loads (ds_read_b64), which the compiler neither
+// hoists out of the spin nor merges, and whose lgkmcnt waits it tracks itself.
+__device__ __forceinline__ uint64_t lds_load64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint64_t pack(uint32_t tag, float v) {
+    return ((uint64_t)tag << 32) | __builtin_bit_cast(uint32_t, v);
+}
+// Lane 63 alone stores both words (EXEC narrowed inside the asm and restored), so the publish
+// neither branches divergently (which would turn the loop counters into VGPRs) nor spends LDS
+// bandwidth on 63 idle lanes.
+__device__ __forceinline__ void publish_lane63(uint32_t addr, uint64_t lo, uint64_t hi) {
+    uint64_t saved;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b32 exec_lo, 0\n\t"
+        "s_mov_b32 exec_hi, 0x80000000\n\t"
+        "s_nop 1\n\t"
+        "ds_write2_b64 %1, %2, %3 offset1:1\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "v"(addr), "v"(lo), "v"(hi)
+        : "memory");
+}
+
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long x;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(x)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return x;
+}
+
+template <int SM, int W, int HA, bool STAMP = false>
+__global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
+    constexpr int HM = kBandHeavy;
+    constexpr uint32_t B = 64 * W;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+
+    const uint32_t n = m.n, erow = m.erow, S = m.S;
+    const uint32_t t = threadIdx.x, lane = t & 63u, q = blockIdx.x;
+    const uint32_t wave = (uint32_t)uniform((int)(t >> 6));
+    constexpr uint32_t tail = SM * B;
+
+    // LDS: heavy constants [kChainMaxSym][kBandTail] | part[kRing][kMaxWaves] | bnd[..] (8 B
+    //      tagged words) | red | symbols [kChainSymChunk]
+    float* ctab = lds;
+    uint64_t* rec = reinterpret_cast<uint64_t*>(lds + kChainMaxSym * kBandTail);  // [kRing][kMaxWaves][2]
+    float* red = reinterpret_cast<float*>(rec + 2 * kRing * kMaxWaves);
+    uint8_t* symr = reinterpret_cast<uint8_t*>(red + 2 * kMaxWaves);
+
+    // ---- resident tables ---------------------------------------------------------------------
+    f32x32 et[SM];  // et[s][o] = E[o][position t*SM+s]
+#pragma unroll
+    for (int s = 0; s < SM; ++s)
+#pragma unroll
+        for (int o = 0; o < kChainMaxSym; ++o)
+            et[s][o] = (uint32_t)o < S ? m.erows[(size_t)o * erow + s * B + t] : kInf;
+    float aw[HA][SM], bw[SM];
+#pragma unroll
+    for (int s = 0; s < SM; ++s) {
+        bw[s] = m.bw[s * B + t];
+#pragma unroll
+        for (int h = 0; h < HA; ++h) aw[h][s] = m.aw[(size_t)h * tail + s * B + t];
+    }
+    for (uint32_t x = t; x < S * kBandTail; x += B)
+        ctab[x] = m.erows[(size_t)(x / kBandTail) * erow + tail + x % kBandTail];
+    for (uint32_t x = t; x < 2 * kRing * kMaxWaves; x += B) rec[x] = 0ull;
+
+    // ---- sequence ----------------------------------------------------------------------------
+    const uint8_t* sym = b.symbols + b.sym_off[q];
+    const uint32_t len = (uint32_t)uniform((int)b.end[q]);
+    uint32_t first = (uint32_t)uniform((int)b.begin[q]);
+    // symbols [sbase, sbase + kChainSymChunk) staged in LDS (16 B aligned, zero padded source)
+    uint32_t sbase = first & ~15u;
+    auto stage_symbols = [&]() {
+        const uint4* src = reinterpret_cast<const uint4*>(sym + sbase);
+        const uint32_t avail = (len + kSymPad - sbase) / 16;
+        const uint32_t words = min((uint32_t)kChainSymChunk / 16, avail);
+        for (uint32_t x = t; x < words; x += B) reinterpret_cast<uint4*>(symr)[x] = src[x];
+    };
+    stage_symbols();
+    __syncthreads();  // symbols, constants and tags initialised: the only barrier before the epilogue
+    float v[SM], vh[HM];
+    if (first == 0) {
+        const uint32_t o0 = (uint32_t)uniform((int)symr[0]);
+#pragma unroll
+        for (int s = 0; s < SM; ++s) v[s] = et[s][o0] + m.start[s * B + t];  // diag(E[s0]) (x) start
+#pragma unroll
+        for (int h = 0; h < HM; ++h)
+            vh[h] = m.hvalid[h] ? ctab[o0 * kBandTail + kBandTailE + h] + m.hstart[h] : kInf;
+        first = 1;
+    } else {
+        const float* vin = b.v_in + (size_t)b.v_in_row[q] * n;
+#pragma unroll
+        for (int s = 0; s < SM; ++s) {
+            const uint32_t r = m.lrow[s * B + t];
+            v[s] = r != 0xFFFFFFFFu ? vin[r] : kInf;
+        }
+#pragma unroll
+        for (int h = 0; h < HM; ++h) vh[h] = m.hvalid[h] ? vin[m.hrow[h]] : kInf;
+    }
+
+    unsigned long long st_acc[kBandStamps] = {};
+    unsigned long long st_prev = 0;
+    auto mark = [&](int seg) {
+        if constexpr (STAMP) {
+            const unsigned long long now = stamp();
+            st_acc[seg] += now - st_prev;
+            st_prev = now;
+        }
+    };
+    if constexpr (STAMP) st_prev = stamp();
+
+    auto wave_partial = [&](const float* vv) -> float {
+        float pm = vv[0];
+#pragma unroll
+        for (int s = 1; s < SM; ++s) pm = fminf(pm, vv[s]);
+        return wave_min63(pm);
+    };
+    // rec[k % kRing][wave] = {partial of observation k, k+1 | last score of the wave at k, k+1}:
+    // the partial is read by every wave at k+2, the last score by wave+1 at k+1.
+    auto publish = [&](uint32_t obs, float partial, float vlast) {
+        publish_lane63(lds_addr(rec + 2 * ((obs & (kRing - 1)) * kMaxWaves + wave)), pack(obs + 1u, partial),
+                       pack(obs + 1u, vlast));
+    };
+    // Bounded spins: `spins` is wave-uniform (every decision goes through readfirstlane).
+    uint32_t spins = 0;
+    // min over every wave's partial of observation obs; `w` holds a first read of the words
+    auto take_mu = [&](uint32_t obs, uint64_t (&w)[W]) -> float {
+        const uint64_t* pw = rec + 2 * (obs & (kRing - 1)) * kMaxWaves;
+        float mu;
+        while (true) {
+            uint32_t tmin = 0xFFFFFFFFu;
+            mu = kInf;
+#pragma unroll
+            for (int x = 0; x < W; ++x) {
+                tmin = min(tmin, (uint32_t)(w[x] >> 32));
+                mu = fminf(mu, __builtin_bit_cast(float, (uint32_t)w[x]));
+            }
+            if (__builtin_expect(uniform((int)tmin) == (int)(obs + 1u), 1)) break;
+            if (++spins > kSpinLimit) break;
+            if (!(m.dbg & 8u)) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int x = 0; x < W; ++x) w[x] = lds_load64(pw + 2 * x);
+        }
+        return mu;
+    };
+    // the left neighbour's last score of observation obs; `w` holds a first read of the word
+    auto take_bnd = [&](uint32_t obs, uint64_t w) -> float {
+        if (W == 1 || wave == 0) return kInf;
+        const uint64_t* bp = rec + 2 * ((obs & (kRing - 1)) * kMaxWaves + wave - 1) + 1;
+        while (true) {
+            if (__builtin_expect(uniform((int)(uint32_t)(w >> 32)) == (int)(obs + 1u), 1)) break;
+            if (++spins > kSpinLimit) break;
+            if (!(m.dbg & 8u)) __builtin_amdgcn_s_sleep(1);
+            w = lds_load64(bp);
+        }
+        return __builtin_bit_cast(float, (uint32_t)w);
+    };
+    // heavy constants of symbol o (read one observation before they are needed)
+    struct HeavyConst {
+        float4 c0;
+        float2 c1;
+    };
+    auto load_heavy = [&](uint32_t o) -> HeavyConst {
+        return {*reinterpret_cast<const float4*>(ctab + o * kBandTail),
+                *reinterpret_cast<const float2*>(ctab + o * kBandTail + 4)};
+    };
+    // heavy scores from mu (partials) and their previous values
+    auto heavy_update = [&](float mu, const HeavyConst& hc) {
+        const float cst[6] = {hc.c0.x, hc.c0.y, hc.c0.z, hc.c0.w, hc.c1.x, hc.c1.y};
+        float vhn[HM];
+#pragma unroll
+        for (int h = 0; h < HM; ++h) {
+            float a = cst[kBandTailA + h] + mu;
+#pragma unroll
+            for (int k = 0; k < HM; ++k) a = fminf(a, cst[kBandTailX + h * HM + k] + vh[k]);
+            vhn[h] = a;
+        }
+#pragma unroll
+        for (int h = 0; h < HM; ++h) vh[h] = vhn[h];
+    };
+
+    // One observation i with symbol o.  hc_prev: heavy constants of the symbol of i-1.  Order:
+    // everything that does not need another wave first; the wave's last score is published before
+    // the left neighbour's boundary is consumed (only lane 0's slot 0 needs it), so every exchange
+    // has at least one observation of slack.  Returns the heavy constants of o.
+    auto step = [&](uint32_t i, uint32_t o, const HeavyConst& hc_prev) -> HeavyConst {
+        mark(0);
+        const bool lagged = i > first;  // uniform: the partials of i-2 exist
+        uint64_t pwv[W];
+        if (lagged) {
+            const uint64_t* pw = rec + 2 * ((i - 2) & (kRing - 1)) * kMaxWaves;
+#pragma unroll
+            for (int x = 0; x < W; ++x) pwv[x] = lds_load64(pw + 2 * x);
+        }
+        const uint64_t bwv = lds_load64(rec + 2 * (((i - 1) & (kRing - 1)) * kMaxWaves + (wave ? wave - 1 : 0)) + 1);
+        const HeavyConst hc = load_heavy(o);
+        // E[o] of the thread's positions: one indexed-register block (s_set_gpr_idx_on .. off)
+        float e[SM];
+#pragma unroll
+        for (int s = 0; s < SM; ++s) e[s] = et[s][o];
+        pin(e);  // all SM extractions adjacent: one s_set_gpr_idx_on .. off block
+        // terms that do not need the heavy scores (lane 0's slot 0 is redone below)
+        const float p0 = wave_shr1(v[SM - 1], kInf);
+        float xb[SM], xa[HA][SM];
+#pragma unroll
+        for (int s = 0; s < SM; ++s) {
+            xb[s] = (e[s] + bw[s]) + (s == 0 ? p0 : v[s - 1]);
+#pragma unroll
+            for (int h = 0; h < HA; ++h) xa[h][s] = e[s] + aw[h][s];
+        }
+        mark(1);
+        if (lagged) heavy_update(take_mu(i - 2, pwv), hc_prev);  // heavy scores of i-1
+        mark(2);
+        float vn[SM];
+#pragma unroll
+        for (int s = 0; s < SM; ++s) {
+            float r = xb[s];
+#pragma unroll
+            for (int h = 0; h < HA; ++h) r = fminf(r, xa[h][s] + vh[h]);
+            vn[s] = r;
+        }
+        mark(3);
+        // lane 0, slot 0: the chain predecessor is the left neighbour's last score of i-1
+        {
+            const float bv = take_bnd(i - 1, bwv);
+            float r = (e[0] + bw[0]) + bv;
+#pragma unroll
+            for (int h = 0; h < HA; ++h) r = fminf(r, xa[h][0] + vh[h]);
+            vn[0] = lane == 0 ? r : vn[0];
+        }
+        publish(i, wave_partial(vn), vn[SM - 1]);
+        mark(4);
+#pragma unroll
+        for (int s = 0; s < SM; ++s) v[s] = vn[s];
+        return hc;
+    };
+
+    publish(first - 1, wave_partial(v), v[SM - 1]);
+    auto sym_word = [&](uint32_t i) -> uint32_t {  // symbols i .. i+3 (i % 4 == 0)
+        return *reinterpret_cast<const uint32_t*>(symr + (i - sbase));
+    };
+    uint32_t i = first;
+    HeavyConst hc = {};
+    // head: single steps up to a multiple of 4
+    for (; i < len && (i & 3u); i = (uint32_t)uniform((int)(i + 1))) {
+        const uint32_t o = (uint32_t)uniform((int)symr[i - sbase]);
+        hc = step(i, o, hc);
+    }
+    // body: groups of four observations, one symbol word each
+    if (i + 4 <= len) {
+        uint32_t word = (uint32_t)uniform((int)sym_word(i));
+        for (; i + 4 <= len; i = (uint32_t)uniform((int)(i + 4))) {
+            if (__builtin_expect(i + 8 > sbase + kChainSymChunk, 0)) {  // uniform: refill (rare)
+                __syncthreads();  // every wave is at observation i: the old chunk is dead
+                sbase = i & ~15u;
+                stage_symbols();
+                __syncthreads();
+                word = (uint32_t)uniform((int)sym_word(i));
+            }
+            const uint32_t next = sym_word(i + 4);  // zero padding past len; retired next group
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t o = (uint32_t)uniform((int)((word >> (8 * k)) & 0xFFu));
+                hc = step(i + k, o, hc);
+            }
+            word = (uint32_t)uniform((int)next);
+        }
+    }
+    // tail
+    for (; i < len; i = (uint32_t)uniform((int)(i + 1))) {
+        const uint32_t o = (uint32_t)uniform((int)symr[i - sbase]);
+        hc = step(i, o, hc);
+    }
+    if (len > first) {  // heavy scores of the last observation (partials of len-2)
+        const uint64_t* pw = rec + 2 * ((len - 2) & (kRing - 1)) * kMaxWaves;
+        uint64_t pwv[W];
+#pragma unroll
+        for (int x = 0; x < W; ++x) pwv[x] = lds_load64(pw + 2 * x);
+        heavy_update(take_mu(len - 2, pwv), hc);
+    }
+
+    if constexpr (STAMP) {
+        if (lane == 0 && m.stamps) {
+            mark(5);
+            st_acc[6] = spins;
+            for (int k = 0; k < kBandStamps; ++k)
+                m.stamps[((size_t)q * kMaxWaves + wave) * kBandStamps + k] = st_acc[k];
+        }
+    }
+    if (spins > kSpinLimit && lane == 0 && m.fault) atomicOr(m.fault, 1u);
+
+    // ---- epilogue: scores and the lowest-index argmin ---------------------------------------
+    float* out = b.scores + (size_t)q * n;
+    float bvv = kInf;
+    uint32_t bk = 0xFFFFFFFFu;
+#pragma unroll
+    for (int s = 0; s < SM; ++s) {
+        const uint32_t r = m.lrow[s * B + t];
+        if (r != 0xFFFFFFFFu) {
+            out[r] = v[s];
+            lex_min(bvv, bk, v[s], r);
+        }
+    }
+    if (t < (uint32_t)HM && m.hvalid[t]) out[m.hrow[t]] = t ? vh[1] : vh[0];
+    if (t == 0) {
+#pragma unroll
+        for (int h = 0; h < HM; ++h)
+            if (m.hvalid[h]) lex_min(bvv, bk, vh[h], (uint32_t)m.hrow[h]);
+    }
+    wave_lexmin63(bvv, bk);
+    uint32_t* redk = reinterpret_cast<uint32_t*>(red + kMaxWaves);
+    if (lane == 63) {
+        red[wave] = bvv;
+        redk[wave] = bk;
+    }
+    __syncthreads();
+    if (t == 0 && b.best) {
+        float fv = red[0];
+        uint32_t fk = redk[0];
+        for (uint32_t w = 1; w < (uint32_t)W; ++w) lex_min(fv, fk, red[w], redk[w]);
+        b.best[q] = (fk == 0xFFFFFFFFu) ? -1 : (int64_t)fk;
+    }
+}
+
+// Instantiated geometries: W waves x SM slots (positions <= 64*W*SM).
+template <int W, int HA>
+const void* chain_ptr_w(int sm) {
+    if (sm > 5) return nullptr;  // 6 slots x 32 symbols would spill past 256 VGPRs
+    switch (sm) {
+#define SVH_CASE(SMV) \
+    case SMV: return reinterpret_cast<const void*>(&chain_viterbi_kernel<SMV, W, HA>);
+        SVH_CASE(1) SVH_CASE(2) SVH_CASE(3) SVH_CASE(4) SVH_CASE(5) SVH_CASE(6)
+#undef SVH_CASE
+        default: return nullptr;
+    }
+}
+template <int HA>
+const void* chain_ptr(int sm, int waves) {
+    switch (waves) {
+        case 1: return chain_ptr_w<1, HA>(sm);
+        case 2: return chain_ptr_w<2, HA>(sm);
+        case 4: return chain_ptr_w<4, HA>(sm);
+        case 8: return chain_ptr_w<8, HA>(sm);
+        default: return nullptr;
+    }
+}
+const void* chain_fn(int sm, int waves, int ha) {
+    return ha == 1 ? chain_ptr<1>(sm, waves) : ha == 2 ? chain_ptr<2>(sm, waves) : nullptr;
+}
+
+}  // namespace
+
+bool chain_supported(int sm, int waves, int ha) { return chain_fn(sm, waves, ha) != nullptr; }
+
+hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStream_t stream) {
+    const int waves = (int)(m.B / 64);
+    const void* fn = chain_fn((int)m.SM, waves, ha);
+    if ((m.dbg & 4u) && m.SM == 5 && waves == 8 && ha == 1)
+        fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, true>);
+    if ((m.dbg & 4u) && m.SM == 5 && waves == 1 && ha == 1)
+        fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 1, 1, true>);
+    if (!fn || m.B % 64 || m.S > (uint32_t)kChainMaxSym || m.erow < m.SM * m.B + kBandTail)
+        return hipErrorInvalidValue;
+    if (b.nseq == 0) return hipSuccess;
+    BandModel mm = m;
+    FusedBatch bb = b;
+    void* args[] = {&mm, &bb};
+    return hipLaunchKernel(fn, dim3(b.nseq), dim3(m.B), args, chain_lds_bytes(), stream);
+}
+
+}  // namespace svh

@@ -59,6 +59,55 @@ struct FusedBatch {
     uint32_t nseq;
 };
 
+// Chain ("band") kernel model: the MSV shape of every reference .chmm (N, M_1..M_L, C).
+//   Light rows (all but <= kBandHeavy heavy rows), in ascending row order at positions p, have
+//   terms only from heavy rows (weights aw) and from the light row at position p-1 (weight bw).
+//   Each heavy row h has one weight w_h shared by ALL light rows (or no light source at all) plus
+//   terms from heavy rows.  Position p = t*SM + s lives in slot s of thread t (blocked); per-thread
+//   tables use the lane-consecutive index s*B + t.
+constexpr int kBandHeavy = 2;
+constexpr int kMaxBandThreads = 1024;
+constexpr int kDefaultBandThreads = 512;
+// Row tail (floats at offset SM*B of every emission row of symbol o):
+//   cA[h]    = fl(E_o[h] + w_h)          the shared uniform term of heavy row h
+//   cX[h][k] = fl(E_o[h] + T^T[h][k])    heavy row k -> heavy row h (+inf if absent)
+//   Eh[h]    = E_o[h]
+constexpr int kBandTailA = 0;
+constexpr int kBandTailX = kBandHeavy;
+constexpr int kBandTailE = kBandHeavy + kBandHeavy * kBandHeavy;
+constexpr int kBandTail = 8;  // floats (>= kBandTailE + kBandHeavy, multiple of 4)
+static_assert(kBandTailE + kBandHeavy <= kBandTail, "band row tail");
+
+struct BandModel {
+    const float* erows;     // [S][erow]: [s*B + t] = E[o][row of position t*SM+s] (+inf pad), tail
+    const float* start;     // [SM*B] start of light positions (+inf pad)
+    const float* aw;        // [HA][SM*B] weight of the term from heavy row h
+    const float* bw;        // [SM*B] weight of the term from position p-1
+    const uint32_t* lrow;   // [SM*B] row id of the position (0xFFFFFFFF pad)
+    int hrow[kBandHeavy];   // heavy row ids (dummy rows: hvalid 0)
+    int hvalid[kBandHeavy];
+    float hstart[kBandHeavy];
+    uint32_t n, S, B, SM, erow, H;
+    uint32_t dbg;  // diagnostic ablations (timing only, wrong results): 1 no DMA, 2 no barrier,
+                   // 4 s_memtime segment stamps into `stamps` (SM=5 HA=1 build only)
+    unsigned long long* stamps;  // [nseq][kMaxWaves][kBandStamps] cycle sums (dbg & 4)
+    uint32_t* fault;             // chain kernel: set non-zero if a bounded spin gave up
+};
+constexpr int kBandStamps = 8;
+
+// Barrier-free chain kernel (chain.hip): emission table in VGPRs (S <= kChainMaxSym), waves
+// synchronise through tagged 64-bit LDS words instead of s_barrier.
+constexpr int kChainMaxSym = 32;
+constexpr int kChainMaxThreads = 512;
+constexpr uint32_t kChainSymChunk = 32768;  // symbols staged in LDS per refill
+inline size_t chain_lds_bytes() {
+    return (size_t)kChainMaxSym * kBandTail * sizeof(float) + 4 * 2 * kMaxWaves * 8 +
+           2 * kMaxWaves * sizeof(float) + kChainSymChunk;
+}
+// Chain kernel for (SM slots, W waves, HA heavy feeders); false if not instantiated.
+bool chain_supported(int sm, int waves, int ha);
+hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStream_t stream);
+
 // CSR of T^T used by the generic kernel and the _spec precompute.
 struct CsrModel {
     const float* emis;       // [S][n]
@@ -109,6 +158,13 @@ constexpr size_t kMaxLdsBytes = 160 * 1024;
 
 hipError_t launch_fused(const FusedModel& m, const FusedBatch& b, int fam, bool paths,
                         hipStream_t stream);
+// Chain kernel (band.hip): slot counts instantiated, LDS bytes, launcher.
+constexpr int kBandSlotChoices[] = {1, 2, 3, 4, 5, 6, 8, 10, 12, 16};
+constexpr int kNumBandSlotChoices = 10;
+inline size_t band_lds_bytes(uint32_t erow) {
+    return (3 * (size_t)erow + 4 * kMaxWaves + 2 * kMaxWaves) * sizeof(float) + kSymChunk + 64 + 16;
+}
+hipError_t launch_band(const BandModel& m, int ha, const FusedBatch& b, hipStream_t stream);
 size_t generic_lds_bytes(uint32_t n);
 hipError_t launch_generic(const CsrModel& m, const FusedBatch& b, int threads, bool paths,
                           hipStream_t stream);

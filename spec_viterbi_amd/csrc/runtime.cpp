@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -288,6 +290,249 @@ Plan make_plan(const HostModel& hm, int max_threads, bool allow_uniform) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Chain ("band") planning: light rows in ascending row order at positions p; each light row's
+// terms come from heavy rows and from position p-1 only; each heavy row's light sources are
+// either all light rows with one shared weight, or none; heavy-row exceptions come from heavy
+// rows only.  Every reference .chmm (MSV shape) qualifies.
+// ------------------------------------------------------------------------------------------
+namespace {
+
+// Heavy rows of the chain plan: rows with in-degree > kBandHeavy + 1, plus (repeatedly) the first light row
+// whose terms break the chain rule, while at most kBandHeavy rows are heavy.
+bool band_heavy_rows(const HostModel& hm, std::vector<uint32_t>* heavy_out) {
+    const uint32_t n = hm.n;
+    std::vector<uint8_t> is_heavy(n, 0);
+    uint32_t count = 0;
+    for (uint32_t j = 0; j < n; ++j)
+        if (hm.rowptr[j + 1] - hm.rowptr[j] > (uint32_t)kBandHeavy + 1) {  // > HA_max + 1 terms
+            is_heavy[j] = 1;
+            ++count;
+        }
+    while (count <= (uint32_t)kBandHeavy) {
+        uint32_t prev = 0xFFFFFFFFu, bad = 0xFFFFFFFFu;
+        for (uint32_t j = 0; j < n && bad == 0xFFFFFFFFu; ++j) {
+            if (is_heavy[j]) continue;
+            for (uint32_t e = hm.rowptr[j]; e < hm.rowptr[j + 1]; ++e) {
+                const uint32_t k = hm.col[e];
+                if (!is_heavy[k] && k != prev) {
+                    bad = j;
+                    break;
+                }
+            }
+            prev = j;
+        }
+        if (bad == 0xFFFFFFFFu) {
+            heavy_out->clear();
+            for (uint32_t j = 0; j < n; ++j)
+                if (is_heavy[j]) heavy_out->push_back(j);
+            return true;
+        }
+        is_heavy[bad] = 1;
+        ++count;
+    }
+    return false;
+}
+
+}  // namespace
+
+BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
+    BandPlan bp;
+    const uint32_t n = hm.n, S = hm.S;
+    if (chain && S > (uint32_t)kChainMaxSym) return bp;
+    if (max_threads <= 0) max_threads = chain ? kChainMaxThreads : kDefaultBandThreads;
+    max_threads = std::min(max_threads, chain ? kChainMaxThreads : kMaxBandThreads);
+    std::vector<uint32_t> heavy;
+    if (!band_heavy_rows(hm, &heavy)) return bp;
+    if (heavy.size() > (size_t)kBandHeavy || heavy.size() >= n) return bp;
+    std::vector<int> hidx(n, -1);
+    for (size_t h = 0; h < heavy.size(); ++h) hidx[heavy[h]] = (int)h;
+    std::vector<uint32_t> light, pos(n, 0xFFFFFFFFu);
+    for (uint32_t j = 0; j < n; ++j)
+        if (hidx[j] < 0) {
+            pos[j] = (uint32_t)light.size();
+            light.push_back(j);
+        }
+    const uint32_t nL = (uint32_t)light.size();
+
+    // light-row terms
+    std::vector<float> bwp(nL, kInfH);
+    std::vector<std::vector<float>> awp(heavy.size(), std::vector<float>(nL, kInfH));
+    std::vector<uint8_t> feeds(heavy.size(), 0);
+    for (uint32_t p = 0; p < nL; ++p) {
+        const uint32_t j = light[p];
+        for (uint32_t e = hm.rowptr[j]; e < hm.rowptr[j + 1]; ++e) {
+            const uint32_t k = hm.col[e];
+            if (hidx[k] >= 0) {
+                awp[hidx[k]][p] = hm.val[e];
+                feeds[hidx[k]] = 1;
+            } else if (p > 0 && pos[k] == p - 1) {
+                bwp[p] = hm.val[e];
+            } else {
+                return bp;
+            }
+        }
+    }
+    // heavy rows: feeders of light rows first (the kernel reads aw[h] against vh[h], h < HA)
+    std::vector<uint32_t> order;
+    for (size_t h = 0; h < heavy.size(); ++h)
+        if (feeds[h]) order.push_back((uint32_t)h);
+    const uint32_t HA = (uint32_t)order.size();
+    for (size_t h = 0; h < heavy.size(); ++h)
+        if (!feeds[h]) order.push_back((uint32_t)h);
+    std::vector<int> newidx(heavy.size());
+    for (size_t x = 0; x < order.size(); ++x) newidx[order[x]] = (int)x;
+
+    float wh[kBandHeavy] = {kInfH, kInfH};
+    std::vector<std::pair<uint32_t, float>> exc[kBandHeavy];
+    for (size_t x = 0; x < order.size(); ++x) {
+        const uint32_t j = heavy[order[x]];
+        uint32_t nlight = 0;
+        bool first = true, same = true;
+        float w = kInfH;
+        for (uint32_t e = hm.rowptr[j]; e < hm.rowptr[j + 1]; ++e) {
+            const uint32_t k = hm.col[e];
+            if (hidx[k] >= 0) {
+                exc[x].push_back({(uint32_t)newidx[hidx[k]], hm.val[e]});
+            } else {
+                ++nlight;
+                if (first) w = hm.val[e];
+                else same &= float_bits(hm.val[e]) == float_bits(w);
+                first = false;
+            }
+        }
+        if (exc[x].size() > (size_t)kBandHeavy) return bp;  // cannot happen: one term per source
+        if (nlight != 0 && (nlight != nL || !same)) return bp;
+        wh[x] = nlight ? w : kInfH;
+    }
+
+    uint32_t SM = 0, B = 0;
+    if (chain) {
+        // barrier-free kernel: fewest waves (1, 2, 4, 8) holding <= 5 positions per thread
+        for (uint32_t w = 1; w <= 8 && SM == 0; w *= 2) {
+            if (64 * w > (uint32_t)max_threads) break;
+            const uint32_t sm = (nL + 64 * w - 1) / (64 * w);
+            if (sm <= 5 || w == 8 || 128 * w > (uint32_t)max_threads) {
+                if (chain_supported((int)sm, (int)w, (int)std::max<uint32_t>(HA, 1))) {
+                    SM = sm;
+                    B = 64 * w;
+                }
+                break;
+            }
+        }
+    } else {
+        // barrier kernel: fewest slots per thread within the thread cap
+        for (int c = 0; c < kNumBandSlotChoices; ++c) {
+            const uint32_t sm = (uint32_t)kBandSlotChoices[c];
+            const uint32_t b = std::max<uint32_t>(64, round_up((nL + sm - 1) / sm, 64));
+            if (b > (uint32_t)max_threads) continue;
+            SM = sm;
+            B = b;
+            break;
+        }
+    }
+    if (SM == 0) return bp;
+    const uint32_t cap = SM * B;
+    const uint32_t erow = round_up(cap + kBandTail, 256);
+    if (band_lds_bytes(erow) > kMaxLdsBytes) return bp;
+
+    bp.ok = true;
+    bp.chain = chain;
+    bp.B = B;
+    bp.SM = SM;
+    bp.HA = HA;
+    bp.H = (uint32_t)heavy.size();
+    bp.nL = nL;
+    bp.erow = erow;
+    bp.lds_bytes = band_lds_bytes(erow);
+    for (int x = 0; x < kBandHeavy; ++x) {
+        const bool real = (size_t)x < order.size();
+        bp.hrow[x] = real ? (int)heavy[order[x]] : 0;
+        bp.hvalid[x] = real ? 1 : 0;
+        bp.hstart[x] = real ? hm.start[heavy[order[x]]] : kInfH;
+    }
+    // per-thread tables, lane-consecutive index s*B + t for position t*SM + s
+    auto slot_of = [&](uint32_t p) { return (p % SM) * B + p / SM; };
+    bp.lrow.assign(cap, 0xFFFFFFFFu);
+    bp.start.assign(cap, kInfH);
+    bp.bw.assign(cap, kInfH);
+    bp.aw.assign((size_t)std::max<uint32_t>(HA, 1) * cap, kInfH);
+    for (uint32_t p = 0; p < nL; ++p) {
+        const uint32_t x = slot_of(p);
+        bp.lrow[x] = light[p];
+        bp.start[x] = hm.start[light[p]];
+        bp.bw[x] = bwp[p];
+        for (uint32_t a = 0; a < HA; ++a) bp.aw[(size_t)a * cap + x] = awp[order[a]][p];
+    }
+    // emission rows: permuted light part, then the folded heavy constants
+    bp.erows.assign((size_t)S * erow, kInfH);
+    for (uint32_t o = 0; o < S; ++o) {
+        const float* E = hm.emis.data() + (size_t)o * n;
+        float* row = bp.erows.data() + (size_t)o * erow;
+        for (uint32_t p = 0; p < nL; ++p) row[slot_of(p)] = E[light[p]];
+        float* tl = row + cap;
+        for (int x = 0; x < kBandHeavy; ++x) {
+            if (!bp.hvalid[x]) continue;
+            const float eh = E[bp.hrow[x]];
+            tl[kBandTailA + x] = eh + wh[x];  // fl(E_h + w_h): the shared uniform term
+            for (const auto& [src, w] : exc[x]) tl[kBandTailX + x * kBandHeavy + src] = eh + w;  // heavy src -> h
+            tl[kBandTailE + x] = eh;
+        }
+    }
+    return bp;
+}
+
+void DeviceBandPlan::upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream_t s) {
+    plan = p;
+    if (!p.ok) return;
+    d_erows.upload(p.erows.data(), p.erows.size() * 4, s);
+    d_start.upload(p.start.data(), p.start.size() * 4, s);
+    d_aw.upload(p.aw.data(), p.aw.size() * 4, s);
+    d_bw.upload(p.bw.data(), p.bw.size() * 4, s);
+    d_lrow.upload(p.lrow.data(), p.lrow.size() * 4, s);
+    std::memset(&view, 0, sizeof(view));
+    view.erows = d_erows.as<float>();
+    view.start = d_start.as<float>();
+    view.aw = d_aw.as<float>();
+    view.bw = d_bw.as<float>();
+    view.lrow = d_lrow.as<uint32_t>();
+    for (int h = 0; h < kBandHeavy; ++h) {
+        view.hrow[h] = p.hrow[h];
+        view.hvalid[h] = p.hvalid[h];
+        view.hstart[h] = p.hstart[h];
+    }
+    view.n = n;
+    view.S = S;
+    view.B = p.B;
+    view.SM = p.SM;
+    view.erow = p.erow;
+    view.H = p.H;
+    d_fault.alloc(4);
+    hip_check(hipMemsetAsync(d_fault.ptr, 0, 4, s), "fault word");
+    view.fault = d_fault.as<uint32_t>();
+    const char* dbg = std::getenv("SVH_BAND_DEBUG");  // diagnostic ablations only
+    view.dbg = dbg ? (uint32_t)std::atoi(dbg) : 0u;
+    if (view.dbg & 4u) {
+        d_stamps.alloc((size_t)4096 * kMaxWaves * kBandStamps * 8);
+        hip_check(hipMemsetAsync(d_stamps.ptr, 0, d_stamps.bytes, s), "stamps");
+        view.stamps = d_stamps.as<unsigned long long>();
+    }
+}
+
+void DeviceBandPlan::report_stamps(uint32_t nseq) const {
+    if (!(view.dbg & 4u) || !view.stamps) return;
+    std::vector<unsigned long long> h((size_t)nseq * kMaxWaves * kBandStamps);
+    if (hipMemcpy(h.data(), view.stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    double sum[kBandStamps] = {};
+    uint32_t cnt = 0;
+    for (uint32_t q = 0; q < nseq; ++q)
+        for (uint32_t w = 0; w < std::max<uint32_t>(plan.B / 64, 1); ++w, ++cnt)
+            for (int k = 0; k < kBandStamps; ++k) sum[k] += (double)h[((size_t)q * kMaxWaves + w) * kBandStamps + k];
+    std::fprintf(stderr, "band stamps (avg cycles per wave over the launch):");
+    for (int k = 0; k < kBandStamps; ++k) std::fprintf(stderr, " s%d=%.0f", k, sum[k] / cnt);
+    std::fprintf(stderr, "\n");
+}
+
+// ------------------------------------------------------------------------------------------
 // Model
 // ------------------------------------------------------------------------------------------
 void DevicePlan::upload(const Plan& p, hipStream_t s) {
@@ -328,12 +573,23 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
     if (dev < 0) hip_check(hipGetDevice(&dev), "hipGetDevice");
     device = dev;
     kernel_pref = opts ? opts->kernel : SVH_KERNEL_AUTO;
-    const int max_threads = (opts && opts->max_threads > 0) ? opts->max_threads : kMaxFusedThreads;
-    if (max_threads % 64 != 0 || max_threads > kMaxFusedThreads)
-        throw Error(SVH_E_INVALID, "max_threads must be a multiple of 64 in [64, 512]");
+    // 0 = each planner's default; the fused kernel caps at kMaxFusedThreads, the chain kernel at
+    // kMaxBandThreads.
+    const int max_threads = (opts && opts->max_threads > 0) ? opts->max_threads : 0;
+    if (max_threads % 64 != 0 || max_threads > std::max(kMaxFusedThreads, kMaxBandThreads))
+        throw Error(SVH_E_INVALID, "max_threads must be 0 or a multiple of 64 in [64, 1024]");
     DeviceGuard g(device);
     hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
 
+    if (kernel_pref == SVH_KERNEL_AUTO || kernel_pref == SVH_KERNEL_BAND || kernel_pref == SVH_KERNEL_CHAIN) {
+        BandPlan bpl;
+        if (kernel_pref != SVH_KERNEL_BAND) bpl = make_band_plan(host, max_threads, true);
+        if (!bpl.ok && kernel_pref != SVH_KERNEL_CHAIN) bpl = make_band_plan(host, max_threads, false);
+        if (kernel_pref != SVH_KERNEL_AUTO && !bpl.ok)
+            throw Error(SVH_E_UNSUPPORTED, "chain kernel requested but the model is not chain-shaped "
+                                           "(or too large / too many symbols for it)");
+        band.upload(bpl, host.n, host.S, stream);
+    }
     Plan fast = make_plan(host, max_threads, true);
     fast_plan.upload(fast, stream);
     if (fast.fused) {
@@ -387,6 +643,12 @@ CsrModel Model::csr_view() const {
     c.S = host.S;
     c.nnz = host.nnz();
     return c;
+}
+
+const DeviceBandPlan* Model::band_for(bool paths) const {
+    if (paths || !band.plan.ok) return nullptr;
+    return (kernel_pref == SVH_KERNEL_AUTO || kernel_pref == SVH_KERNEL_BAND ||
+            kernel_pref == SVH_KERNEL_CHAIN) ? &band : nullptr;
 }
 
 const DevicePlan* Model::plan_for(bool paths) const {
@@ -446,7 +708,8 @@ svh_model_info Model::info() const {
     svh_model_info i;
     std::memset(&i, 0, sizeof(i));
     const DevicePlan* p = plan_for(false);
-    i.kernel = p ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
+    const DeviceBandPlan* bpl = band_for(false);
+    i.kernel = bpl ? (bpl->plan.chain ? SVH_KERNEL_CHAIN : SVH_KERNEL_BAND) : p ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
     i.family = p ? p->plan.family : -1;
     i.threads = p ? (int32_t)p->plan.B : (int32_t)std::min<uint32_t>(1024, round_up(host.n, 64));
     i.slots = p ? (int32_t)p->plan.SM : 0;
@@ -458,6 +721,14 @@ svh_model_info Model::info() const {
     i.S = host.S;
     i.nnz = host.nnz();
     i.lds_bytes = p ? p->plan.lds_bytes : generic_lds_bytes(host.n);
+    if (bpl) {
+        i.threads = (int32_t)bpl->plan.B;
+        i.slots = (int32_t)bpl->plan.SM;
+        i.light_terms = (int32_t)bpl->plan.HA + 1;
+        i.heavy_rows = (int32_t)bpl->plan.H;
+        i.heavy_uniform = 1;
+        i.lds_bytes = bpl->plan.chain ? chain_lds_bytes() : bpl->plan.lds_bytes;
+    }
     i.spec_level = spec_level;
     i.spec_bytes = d_products.bytes;
     return i;
@@ -556,7 +827,16 @@ void Batch::run(uint32_t level, hipStream_t s) {
     }
     auto launch_step_kernel = [&](const FusedBatch& b, bool want_paths) {
         const DevicePlan* dp = model->plan_for(want_paths);
-        if (dp) {
+        const DeviceBandPlan* bpl = model->band_for(want_paths);
+        if (bpl) {
+            const int ha = (int)std::max<uint32_t>(bpl->plan.HA, 1);
+            if (bpl->plan.chain) hip_check(launch_chain(bpl->view, ha, b, s), "chain Viterbi kernel");
+            else hip_check(launch_band(bpl->view, ha, b, s), "band Viterbi kernel");
+            if (bpl->view.dbg & 4u) {
+                hip_check(hipStreamSynchronize(s), "stamps");
+                bpl->report_stamps(b.nseq);
+            }
+        } else if (dp) {
             hip_check(launch_fused(dp->view, b, dp->plan.family, want_paths, s), "fused Viterbi kernel");
         } else {
             const uint32_t threads = std::min<uint32_t>(1024, ((model->host.n + 63) / 64) * 64);
@@ -621,6 +901,11 @@ void Batch::read(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out
     if (!ran) throw Error(SVH_E_STATE, "svh_batch_read before svh_batch_run");
     if (paths_out && !paths) throw Error(SVH_E_STATE, "batch was created without SVH_BATCH_PATHS");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (model->band.plan.ok && model->band.view.fault) {
+        uint32_t fault = 0;
+        hip_check(hipMemcpy(&fault, model->band.view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
+        if (fault) throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
+    }
     if (scores)
         hip_check(hipMemcpy(scores, d_scores.ptr, (size_t)nseq * model->host.n * 4, hipMemcpyDeviceToHost),
                   "scores D2H");

@@ -93,12 +93,36 @@ struct DevicePlan {
     void upload(const Plan& p, hipStream_t s);
 };
 
+// Host schedule of the chain ("band") kernel (band.hip); ok == false when the model does not
+// have the chain + uniform-heavy shape.
+struct BandPlan {
+    bool ok = false;
+    bool chain = false;  // barrier-free register kernel (chain.hip) instead of band.hip
+    uint32_t B = 0, SM = 0, HA = 0, H = 0, nL = 0, erow = 0;
+    int hrow[kBandHeavy] = {0, 0};
+    int hvalid[kBandHeavy] = {0, 0};
+    float hstart[kBandHeavy] = {0, 0};
+    std::vector<float> erows, start, aw, bw;
+    std::vector<uint32_t> lrow;
+    size_t lds_bytes = 0;
+};
+BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain);
+
+struct DeviceBandPlan {
+    BandPlan plan;
+    DeviceBuffer d_erows, d_start, d_aw, d_bw, d_lrow, d_stamps, d_fault;
+    BandModel view{};
+    void upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream_t s);
+    void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_BAND_DEBUG & 4)
+};
+
 struct Model {
     std::mutex mu;
     int device = 0;
     int kernel_pref = SVH_KERNEL_AUTO;
     HostModel host;
     hipStream_t stream = nullptr;
+    DeviceBandPlan band;             // chain kernel plan (scores-only runs of MSV-shaped models)
     DevicePlan fast_plan;            // fastest fused plan (may use uniform heavy rows)
     DevicePlan paths_plan_storage;   // term-by-term plan when fast_plan is uniform
     const DevicePlan* paths_plan = nullptr;
@@ -113,6 +137,8 @@ struct Model {
     CsrModel csr_view() const;
     // Fused plan to run (nullptr: generic kernel).
     const DevicePlan* plan_for(bool paths) const;
+    // Chain plan to run for scores-only passes (nullptr: use plan_for(false)).
+    const DeviceBandPlan* band_for(bool paths) const;
     void spec_build(uint32_t level, hipStream_t s);
     svh_model_info info() const;
 };

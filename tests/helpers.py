@@ -90,3 +90,51 @@ def random_hmm(n, S=20, out_degree=3, nstart=2, seed=0, dense_rows=(), self_loop
 def random_seqs(S, lengths, seed=0):
     rng = np.random.default_rng(seed)
     return [rng.integers(0, S, size=int(L)).astype(np.uint64) for L in lengths]
+
+
+def random_chain_hmm(L, S=20, seed=0, self_n=True, self_c=True, feed_c=False, c_from_m=True, n_from_m=True,
+                     zero_emis=0.0, gap=None, start=(0,), **_):
+    """MSV-shaped random model (the shape chmm_files/silent_hmm_to_chmm.py writes): N=0, M_1..M_L,
+    C=L+1.  N -> M_j, M_j -> M_{j+1}, M_j -> N and M_j -> C with one shared weight each, N and C
+    self loops.  Variants: feed_c adds C -> M_j (light rows fed by two heavy rows); c_from_m /
+    n_from_m drop the uniform M -> heavy terms; gap drops M_gap -> M_gap+1 (chain break)."""
+    from spec_viterbi_amd import HMM
+
+    rng = np.random.default_rng(seed)
+    n = L + 2
+    C = L + 1
+    src, dst, pr = [], [], []
+
+    def add(a, b, p):
+        src.append(a)
+        dst.append(b)
+        pr.append(np.float32(p))
+
+    w_n, w_c = rng.uniform(0.01, 0.2), rng.uniform(0.01, 0.2)
+    for j in range(1, L + 1):
+        add(0, j, rng.uniform(0.001, 0.05))
+        if feed_c:
+            add(C, j, rng.uniform(0.001, 0.05))
+        if j < L and j != gap:
+            add(j, j + 1, rng.uniform(0.3, 0.9))
+        if n_from_m:
+            add(j, 0, w_n)
+        if c_from_m:
+            add(j, C, w_c)
+    if self_n:
+        add(0, 0, rng.uniform(0.5, 0.99))
+    if self_c:
+        add(C, C, rng.uniform(0.5, 0.99))
+    em = rng.uniform(0.001, 1.0, size=(S, n)).astype(np.float32)
+    if zero_emis > 0:
+        em[rng.random(em.shape) < zero_emis] = 0.0
+
+    def mod(p):
+        p = np.asarray(p, np.float32)
+        with np.errstate(divide="ignore"):
+            return np.where(p > 0, -np.log2(p), np.inf).astype(np.float32)
+
+    st = np.array(start, np.uint64)
+    return HMM(states_num=n, emit_num=S, trans_num=len(pr), trans_rows=np.array(src, np.uint64),
+               trans_cols=np.array(dst, np.uint64), trans_probs=mod(pr), emissions=mod(em),
+               start_probabilities_cols=st, start_probabilities=mod(rng.uniform(0.1, 1.0, size=st.size)))

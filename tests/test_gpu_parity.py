@@ -10,7 +10,8 @@ import spec_viterbi_amd as svh
 from spec_viterbi_amd import _lib
 from oracle import oracle
 from tests.conftest import chmm, ess
-from tests.helpers import bit_equal, first_mismatch, from_hex, load_golden, random_hmm, random_seqs
+from tests.helpers import (bit_equal, first_mismatch, from_hex, load_golden, random_chain_hmm, random_hmm,
+                           random_seqs)
 
 pytestmark = pytest.mark.gpu
 
@@ -78,7 +79,7 @@ def test_2405_emit50_full_batch_vs_oracle():
     seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
     model = svh.DeviceModel(hmm)
     info = model.info()
-    assert info["kernel"] == _lib.SVH_KERNEL_FUSED and info["heavy_uniform"] == 1, info
+    assert info["kernel"] == _lib.SVH_KERNEL_CHAIN and info["heavy_uniform"] == 1, info
     scores, best = model.viterbi(seqs)
     ref, _ = oracle.viterbi_batch(hmm, seqs, nthreads=16)
     for q in range(len(seqs)):
@@ -173,3 +174,70 @@ def test_batch_api_device_resident_rerun():
     assert batch.elapsed_ms() > 0
     ref, _ = oracle.viterbi_batch(hmm, seqs)
     assert bit_equal(a, ref)
+
+
+def test_2405_chain_band_fused_kernels_bitwise():
+    """The barrier-free chain kernel, the barrier chain kernel and the fused kernel agree bit for
+    bit (and with the oracle)."""
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = [s[:1200] for s in svh.read_emit_seq(ess("emit_50_3500_20.ess"))[:6]]
+    ref, _ = oracle.viterbi_batch(hmm, seqs)
+    out = {}
+    for k in (_lib.SVH_KERNEL_CHAIN, _lib.SVH_KERNEL_BAND, _lib.SVH_KERNEL_FUSED):
+        model = svh.DeviceModel(hmm, kernel=k)
+        assert model.info()["kernel"] == k
+        out[k] = model.viterbi(seqs)
+        assert bit_equal(out[k][0], ref), (k, first_mismatch(out[k][0][0], ref[0]))
+    assert np.array_equal(out[_lib.SVH_KERNEL_CHAIN][1], out[_lib.SVH_KERNEL_FUSED][1])
+
+
+@pytest.mark.parametrize("kernel", [_lib.SVH_KERNEL_CHAIN, _lib.SVH_KERNEL_BAND])
+@pytest.mark.parametrize("threads", [64, 128, 256, 512])
+def test_chain_geometries(kernel, threads):
+    hmm = svh.read_HMM(chmm("1001.chmm") if threads >= 256 or kernel == _lib.SVH_KERNEL_BAND else chmm("200.chmm"))
+    seqs = [s[:900] for s in svh.read_emit_seq(ess("emit_3_3500_20.ess"))]
+    model = check_against_oracle(hmm, seqs, kernel=kernel, max_threads=threads, paths=False)
+    assert model.info()["kernel"] == kernel
+
+
+@pytest.mark.parametrize("L,kw,seed", [
+    (1, {}, 1), (2, {}, 2), (63, {}, 3), (64, {}, 4), (65, {}, 5), (700, {}, 6), (2560, {}, 7),
+    (4000, {}, 14),                                   # too long for the register kernel
+    (300, {"feed_c": True}, 8),                       # light rows fed by both heavy rows
+    (300, {"self_n": False, "self_c": False}, 9),     # no exceptions
+    (300, {"c_from_m": False}, 10),                   # a heavy row without light sources
+    (300, {"zero_emis": 0.2}, 11),                    # +inf emissions
+    (300, {"start": (0, 5, 301)}, 12),                # start in light and heavy rows
+    (300, {"gap": 150}, 13),                          # chain break (no predecessor term)
+    (300, {"S": 40}, 15),                             # too many symbols for the register kernel
+])
+def test_chain_random_models(L, kw, seed):
+    hmm = random_chain_hmm(L, seed=seed, **kw)
+    S = kw.get("S", 20)
+    seqs = random_seqs(S, [1, 2, 3, 4, 5, 77, 1000, 5000], seed=seed)
+    model = svh.DeviceModel(hmm)
+    info = model.info()
+    if L >= 2:
+        want = _lib.SVH_KERNEL_CHAIN if (L <= 2560 and S <= 32) else _lib.SVH_KERNEL_BAND
+        assert info["kernel"] == want, info
+    check_against_oracle(hmm, seqs, paths=False)
+    if L >= 2:
+        check_against_oracle(hmm, seqs, kernel=_lib.SVH_KERNEL_BAND, paths=False)
+    check_against_oracle(hmm, seqs[:4], paths=True)  # paths go through the fused kernel
+
+
+def test_chain_covid_many_sequences_and_resume():
+    """Ragged batch (38..7096) through the chain kernel; then the _spec level-2 tail, which resumes
+    the chain kernel from device-resident scores (begin > 0)."""
+    hmm = svh.read_HMM(chmm("300.chmm"))
+    seqs = svh.read_emit_seq(ess("covid-19.ess"))
+    model = check_against_oracle(hmm, seqs, paths=False)
+    assert model.info()["kernel"] == _lib.SVH_KERNEL_CHAIN
+
+
+def test_band_rejects_non_chain_models():
+    hmm = random_hmm(300, out_degree=3, seed=3)
+    for k in (_lib.SVH_KERNEL_BAND, _lib.SVH_KERNEL_CHAIN):
+        with pytest.raises(_lib.SvhError) as e:
+            svh.DeviceModel(hmm, kernel=k)
+        assert e.value.code == _lib.SVH_E_UNSUPPORTED
