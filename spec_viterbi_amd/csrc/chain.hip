@@ -33,11 +33,23 @@ typedef float f32x32 __attribute__((ext_vector_type(32)));
 constexpr uint32_t kRing = 4;  // see the ring argument in the step comments
 constexpr uint32_t kSpinLimit = 1u << 22;
 
-// Empty asm that consumes the values: everything computing them is emitted before it.
+// Empty asm that consumes the values: everything computing them is emitted before it (and a
+// load's wait lands here, after the independent work placed before it).
 template <int N>
 __device__ __forceinline__ void pin(float (&x)[N]) {
 #pragma unroll
     for (int k = 0; k < N; ++k) asm volatile("" : "+v"(x[k]));
+}
+template <int N>
+__device__ __forceinline__ void pin_u64(uint64_t (&x)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) asm volatile("" : "+v"(x[k]));
+}
+__device__ __forceinline__ void pin_u64(uint64_t& x) { asm volatile("" : "+v"(x)); }
+
+// The partial min lives in lane 63 after wave_min63: broadcast it as a wave-uniform value.
+__device__ __forceinline__ float uniform_f(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
 
 __device__ __forceinline__ float wave_shr1(float x, float old) {
@@ -63,15 +75,13 @@ __device__ __forceinline__ uint64_t pack(uint32_t tag, float v) {
 __device__ __forceinline__ void publish_lane63(uint32_t addr, uint64_t lo, uint64_t hi) {
     uint64_t saved;
     asm volatile(
-        "s_mov_b64 %0, exec\n\t"
-        "s_mov_b32 exec_lo, 0\n\t"
-        "s_mov_b32 exec_hi, 0x80000000\n\t"
+        "s_and_saveexec_b64 %0, %4\n\t"
         "s_nop 1\n\t"
         "ds_write2_b64 %1, %2, %3 offset1:1\n\t"
         "s_mov_b64 exec, %0"
         : "=&s"(saved)
-        : "v"(addr), "v"(lo), "v"(hi)
-        : "memory");
+        : "v"(addr), "v"(lo), "v"(hi), "s"(0x8000000000000000ull)
+        : "memory", "scc");
 }
 
 __device__ __forceinline__ unsigned long long stamp() {
@@ -82,7 +92,7 @@ __device__ __forceinline__ unsigned long long stamp() {
     return x;
 }
 
-template <int SM, int W, int HA, bool STAMP = false>
+template <int SM, int W, int HA, bool GE, bool STAMP = false>
 __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
     constexpr int HM = kBandHeavy;
     constexpr uint32_t B = 64 * W;
@@ -101,12 +111,41 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     uint8_t* symr = reinterpret_cast<uint8_t*>(red + 2 * kMaxWaves);
 
     // ---- resident tables ---------------------------------------------------------------------
-    f32x32 et[SM];  // et[s][o] = E[o][position t*SM+s]
+    // GE == false: et[s][o] = E[o][position t*SM+s] in VGPRs, picked by s_set_gpr_idx.
+    // GE == true:  E rows streamed from L2, [o][t][NQ] float4 per thread, prefetched 4 ahead.
+    constexpr int NQ = (SM + 3) / 4;
+    f32x32 et[GE ? 1 : SM];
+    if constexpr (!GE) {
 #pragma unroll
-    for (int s = 0; s < SM; ++s)
+        for (int s = 0; s < SM; ++s)
 #pragma unroll
-        for (int o = 0; o < kChainMaxSym; ++o)
-            et[s][o] = (uint32_t)o < S ? m.erows[(size_t)o * erow + s * B + t] : kInf;
+            for (int o = 0; o < kChainMaxSym; ++o)
+                et[s][o] = (uint32_t)o < S ? m.erows[(size_t)o * erow + s * B + t] : kInf;
+    }
+    const float4* __restrict__ er4 = reinterpret_cast<const float4*>(m.erows_t);
+    auto load_e4 = [&](uint32_t o, float4 (&d)[NQ]) {
+#pragma unroll
+        for (int x = 0; x < NQ; ++x) d[x] = er4[((size_t)o * B + t) * NQ + x];
+    };
+    auto e_from4 = [&](const float4 (&d)[NQ], float (&e)[SM]) {
+#pragma unroll
+        for (int s = 0; s < SM; ++s) {
+            const float4 q4 = d[s / 4];
+            e[s] = (s % 4 == 0) ? q4.x : (s % 4 == 1) ? q4.y : (s % 4 == 2) ? q4.z : q4.w;
+        }
+    };
+    // E[o] of the thread's positions
+    auto extract = [&](uint32_t o, float (&e)[SM]) {
+        if constexpr (GE) {
+            float4 d[NQ];
+            load_e4(o, d);
+            e_from4(d, e);
+        } else {
+#pragma unroll
+            for (int s = 0; s < SM; ++s) e[s] = et[s][o];
+            pin(e);  // all SM extractions adjacent: one s_set_gpr_idx_on .. off block
+        }
+    };
     float aw[HA][SM], bw[SM];
 #pragma unroll
     for (int s = 0; s < SM; ++s) {
@@ -135,8 +174,10 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     float v[SM], vh[HM];
     if (first == 0) {
         const uint32_t o0 = (uint32_t)uniform((int)symr[0]);
+        float e0[SM];
+        extract(o0, e0);
 #pragma unroll
-        for (int s = 0; s < SM; ++s) v[s] = et[s][o0] + m.start[s * B + t];  // diag(E[s0]) (x) start
+        for (int s = 0; s < SM; ++s) v[s] = e0[s] + m.start[s * B + t];  // diag(E[s0]) (x) start
 #pragma unroll
         for (int h = 0; h < HM; ++h)
             vh[h] = m.hvalid[h] ? ctab[o0 * kBandTail + kBandTailE + h] + m.hstart[h] : kInf;
@@ -171,41 +212,56 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     };
     // rec[k % kRing][wave] = {partial of observation k, k+1 | last score of the wave at k, k+1}:
     // the partial is read by every wave at k+2, the last score by wave+1 at k+1.
-    auto publish = [&](uint32_t obs, float partial, float vlast) {
-        publish_lane63(lds_addr(rec + 2 * ((obs & (kRing - 1)) * kMaxWaves + wave)), pack(obs + 1u, partial),
-                       pack(obs + 1u, vlast));
+    // Ring slots are passed as values the group loop knows at compile time (i % 4), so record
+    // addresses are constant offsets from two per-wave bases: no scalar address work per step.
+    uint64_t* const rec_w = rec + 2 * wave;                     // this wave's column
+    const uint64_t* const rec_l = rec + 2 * (wave ? wave - 1 : 0) + 1;  // left neighbour's last scores
+    auto publish = [&](uint32_t obs, uint32_t slot, float partial, float vlast) {
+        publish_lane63(lds_addr(rec_w + 2 * kMaxWaves * slot), pack(obs + 1u, partial), pack(obs + 1u, vlast));
     };
     // Bounded spins: `spins` is wave-uniform (every decision goes through readfirstlane).
     uint32_t spins = 0;
-    // min over every wave's partial of observation obs; `w` holds a first read of the words
-    auto take_mu = [&](uint32_t obs, uint64_t (&w)[W]) -> float {
-        const uint64_t* pw = rec + 2 * (obs & (kRing - 1)) * kMaxWaves;
-        float mu;
-        while (true) {
-            uint32_t tmin = 0xFFFFFFFFu;
-            mu = kInf;
+    // min over every wave's partial of observation obs; `w` holds a first read of the words.
+    // Fast path: the first read is current (no loop, no copies of w); slow path: re-read loop.
+    auto reduce_words = [&](const uint64_t (&w)[W], uint32_t& tmin) -> float {
+        tmin = 0xFFFFFFFFu;
+        float mu = kInf;
 #pragma unroll
-            for (int x = 0; x < W; ++x) {
-                tmin = min(tmin, (uint32_t)(w[x] >> 32));
-                mu = fminf(mu, __builtin_bit_cast(float, (uint32_t)w[x]));
-            }
-            if (__builtin_expect(uniform((int)tmin) == (int)(obs + 1u), 1)) break;
-            if (++spins > kSpinLimit) break;
-            if (!(m.dbg & 8u)) __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-            for (int x = 0; x < W; ++x) w[x] = lds_load64(pw + 2 * x);
+        for (int x = 0; x < W; ++x) {
+            tmin = min(tmin, (uint32_t)(w[x] >> 32));
+            mu = fminf(mu, __builtin_bit_cast(float, (uint32_t)w[x]));
         }
         return mu;
     };
-    // the left neighbour's last score of observation obs; `w` holds a first read of the word
-    auto take_bnd = [&](uint32_t obs, uint64_t w) -> float {
+    auto take_mu = [&](uint32_t obs, uint32_t slot, const uint64_t (&w0)[W]) -> float {
+        uint32_t tmin;
+        float mu = reduce_words(w0, tmin);
+        if (__builtin_expect(uniform((int)tmin) != (int)(obs + 1u), 0) && !(m.dbg & 16u)) {
+            const uint64_t* pw = rec + 2 * kMaxWaves * slot;
+            while (true) {
+                if (++spins > kSpinLimit) break;
+                if (!(m.dbg & 8u)) __builtin_amdgcn_s_sleep(1);
+                uint64_t w[W];
+#pragma unroll
+                for (int x = 0; x < W; ++x) w[x] = lds_load64(pw + 2 * x);
+                mu = reduce_words(w, tmin);
+                if (uniform((int)tmin) == (int)(obs + 1u)) break;
+            }
+        }
+        return mu;
+    };
+    // the left neighbour's last score of observation obs; `w0` holds a first read of the word
+    auto take_bnd = [&](uint32_t obs, uint32_t slot, uint64_t w0) -> float {
         if (W == 1 || wave == 0) return kInf;
-        const uint64_t* bp = rec + 2 * ((obs & (kRing - 1)) * kMaxWaves + wave - 1) + 1;
-        while (true) {
-            if (__builtin_expect(uniform((int)(uint32_t)(w >> 32)) == (int)(obs + 1u), 1)) break;
-            if (++spins > kSpinLimit) break;
-            if (!(m.dbg & 8u)) __builtin_amdgcn_s_sleep(1);
-            w = lds_load64(bp);
+        uint64_t w = w0;
+        if (__builtin_expect(uniform((int)(uint32_t)(w >> 32)) != (int)(obs + 1u), 0) && !(m.dbg & 16u)) {
+            const uint64_t* bp = rec_l + 2 * kMaxWaves * slot;
+            while (true) {
+                if (++spins > kSpinLimit) break;
+                if (!(m.dbg & 8u)) __builtin_amdgcn_s_sleep(1);
+                w = lds_load64(bp);
+                if (uniform((int)(uint32_t)(w >> 32)) == (int)(obs + 1u)) break;
+            }
         }
         return __builtin_bit_cast(float, (uint32_t)w);
     };
@@ -233,26 +289,25 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         for (int h = 0; h < HM; ++h) vh[h] = vhn[h];
     };
 
+    float own_p1 = kInf, own_p2 = kInf;  // W == 1: partials of the last two observations
     // One observation i with symbol o.  hc_prev: heavy constants of the symbol of i-1.  Order:
     // everything that does not need another wave first; the wave's last score is published before
     // the left neighbour's boundary is consumed (only lane 0's slot 0 needs it), so every exchange
     // has at least one observation of slack.  Returns the heavy constants of o.
-    auto step = [&](uint32_t i, uint32_t o, const HeavyConst& hc_prev) -> HeavyConst {
+    // k3 == i % 4 and lagged == (i > first), both compile-time constants in the group loop.
+    auto step = [&](uint32_t i, uint32_t k3, bool lagged, uint32_t o, const float (&e)[SM],
+                    const HeavyConst& hc_prev) -> HeavyConst {
         mark(0);
-        const bool lagged = i > first;  // uniform: the partials of i-2 exist
+        const uint32_t s0 = k3 & (kRing - 1), s1 = (k3 + kRing - 1) & (kRing - 1), s2 = (k3 + kRing - 2) & (kRing - 1);
         uint64_t pwv[W];
-        if (lagged) {
-            const uint64_t* pw = rec + 2 * ((i - 2) & (kRing - 1)) * kMaxWaves;
+        if (W > 1 && lagged) {
+            const uint64_t* pw = rec + 2 * kMaxWaves * s2;
 #pragma unroll
             for (int x = 0; x < W; ++x) pwv[x] = lds_load64(pw + 2 * x);
         }
-        const uint64_t bwv = lds_load64(rec + 2 * (((i - 1) & (kRing - 1)) * kMaxWaves + (wave ? wave - 1 : 0)) + 1);
+        uint64_t bwv = 0;  // wave 0 has no left neighbour: no load (a dead load still costs a wait)
+        if (W > 1 && wave) bwv = lds_load64(rec_l + 2 * kMaxWaves * s1);
         const HeavyConst hc = load_heavy(o);
-        // E[o] of the thread's positions: one indexed-register block (s_set_gpr_idx_on .. off)
-        float e[SM];
-#pragma unroll
-        for (int s = 0; s < SM; ++s) e[s] = et[s][o];
-        pin(e);  // all SM extractions adjacent: one s_set_gpr_idx_on .. off block
         // terms that do not need the heavy scores (lane 0's slot 0 is redone below)
         const float p0 = wave_shr1(v[SM - 1], kInf);
         float xb[SM], xa[HA][SM];
@@ -262,8 +317,15 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
 #pragma unroll
             for (int h = 0; h < HA; ++h) xa[h][s] = e[s] + aw[h][s];
         }
+        // the exchange reads were issued first; everything above ran while they were in flight
+        pin(xb);
+        pin(xa[0]);
+        if constexpr (W > 1) {
+            if (lagged) pin_u64(pwv);
+            pin_u64(bwv);
+        }
         mark(1);
-        if (lagged) heavy_update(take_mu(i - 2, pwv), hc_prev);  // heavy scores of i-1
+        if (lagged) heavy_update(W > 1 ? take_mu(i - 2, s2, pwv) : own_p2, hc_prev);  // heavy scores of i-1
         mark(2);
         float vn[SM];
 #pragma unroll
@@ -276,33 +338,47 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         mark(3);
         // lane 0, slot 0: the chain predecessor is the left neighbour's last score of i-1
         {
-            const float bv = take_bnd(i - 1, bwv);
+            const float bv = take_bnd(i - 1, s1, bwv);
             float r = (e[0] + bw[0]) + bv;
 #pragma unroll
             for (int h = 0; h < HA; ++h) r = fminf(r, xa[h][0] + vh[h]);
             vn[0] = lane == 0 ? r : vn[0];
         }
-        publish(i, wave_partial(vn), vn[SM - 1]);
+        const float pi = wave_partial(vn);
+        if constexpr (W > 1) {
+            publish(i, s0, pi, vn[SM - 1]);
+        } else {  // one wave: its own partials are the only ones, keep the last two in registers
+            own_p2 = own_p1;
+            own_p1 = uniform_f(pi);
+        }
         mark(4);
 #pragma unroll
         for (int s = 0; s < SM; ++s) v[s] = vn[s];
         return hc;
     };
 
-    publish(first - 1, wave_partial(v), v[SM - 1]);
+    if constexpr (W > 1) publish(first - 1, (first - 1) & (kRing - 1), wave_partial(v), v[SM - 1]);
+    else own_p1 = uniform_f(wave_partial(v));
     auto sym_word = [&](uint32_t i) -> uint32_t {  // symbols i .. i+3 (i % 4 == 0)
         return *reinterpret_cast<const uint32_t*>(symr + (i - sbase));
     };
     uint32_t i = first;
     HeavyConst hc = {};
-    // head: single steps up to a multiple of 4
-    for (; i < len && (i & 3u); i = (uint32_t)uniform((int)(i + 1))) {
+    // head: single steps up to a multiple of 4 (and past `first`, so group steps are lagged)
+    for (; i < len && ((i & 3u) || i == first); i = (uint32_t)uniform((int)(i + 1))) {
         const uint32_t o = (uint32_t)uniform((int)symr[i - sbase]);
-        hc = step(i, o, hc);
+        float e[SM];
+        extract(o, e);
+        hc = step(i, i & 3u, i > first, o, e, hc);
     }
-    // body: groups of four observations, one symbol word each
+    // body: groups of four observations, one symbol word each; GE: E rows prefetched 4 ahead
     if (i + 4 <= len) {
         uint32_t word = (uint32_t)uniform((int)sym_word(i));
+        float4 eb[GE ? 4 : 1][NQ];
+        if constexpr (GE) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) load_e4((word >> (8 * k)) & 0xFFu, eb[k]);
+        }
         for (; i + 4 <= len; i = (uint32_t)uniform((int)(i + 4))) {
             if (__builtin_expect(i + 8 > sbase + kChainSymChunk, 0)) {  // uniform: refill (rare)
                 __syncthreads();  // every wave is at observation i: the old chunk is dead
@@ -315,7 +391,15 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t o = (uint32_t)uniform((int)((word >> (8 * k)) & 0xFFu));
-                hc = step(i + k, o, hc);
+                float e[SM];
+                if constexpr (GE) {
+                    e_from4(eb[k], e);
+                    // row of observation i+k+4 into the slot just consumed (zero padding: row 0)
+                    load_e4((uint32_t)uniform((int)((next >> (8 * k)) & 0xFFu)), eb[k]);
+                } else {
+                    extract(o, e);
+                }
+                hc = step(i + k, (uint32_t)k, true, o, e, hc);
             }
             word = (uint32_t)uniform((int)next);
         }
@@ -323,14 +407,18 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     // tail
     for (; i < len; i = (uint32_t)uniform((int)(i + 1))) {
         const uint32_t o = (uint32_t)uniform((int)symr[i - sbase]);
-        hc = step(i, o, hc);
+        float e[SM];
+        extract(o, e);
+        hc = step(i, i & 3u, i > first, o, e, hc);
     }
     if (len > first) {  // heavy scores of the last observation (partials of len-2)
-        const uint64_t* pw = rec + 2 * ((len - 2) & (kRing - 1)) * kMaxWaves;
+        const uint64_t* pw = rec + 2 * kMaxWaves * ((len - 2) & (kRing - 1));
         uint64_t pwv[W];
+        if constexpr (W > 1) {
 #pragma unroll
-        for (int x = 0; x < W; ++x) pwv[x] = lds_load64(pw + 2 * x);
-        heavy_update(take_mu(len - 2, pwv), hc);
+            for (int x = 0; x < W; ++x) pwv[x] = lds_load64(pw + 2 * x);
+        }
+        heavy_update(W > 1 ? take_mu(len - 2, (len - 2) & (kRing - 1), pwv) : own_p2, hc);
     }
 
     if constexpr (STAMP) {
@@ -378,42 +466,54 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
 
 // Instantiated geometries: W waves x SM slots (positions <= 64*W*SM).
 template <int W, int HA>
-const void* chain_ptr_w(int sm) {
-    if (sm > 5) return nullptr;  // 6 slots x 32 symbols would spill past 256 VGPRs
-    switch (sm) {
+const void* chain_ptr_w(int sm, bool ge) {
+    if (ge) {
+        switch (sm) {
 #define SVH_CASE(SMV) \
-    case SMV: return reinterpret_cast<const void*>(&chain_viterbi_kernel<SMV, W, HA>);
-        SVH_CASE(1) SVH_CASE(2) SVH_CASE(3) SVH_CASE(4) SVH_CASE(5) SVH_CASE(6)
+    case SMV: return reinterpret_cast<const void*>(&chain_viterbi_kernel<SMV, W, HA, true>);
+            SVH_CASE(1) SVH_CASE(2) SVH_CASE(3) SVH_CASE(4) SVH_CASE(5) SVH_CASE(6) SVH_CASE(8)
+            SVH_CASE(10) SVH_CASE(12)
+#undef SVH_CASE
+            default: return nullptr;
+        }
+    }
+    switch (sm) {  // E in VGPRs: <= 5 slots x 32 symbols (6 would spill past 256 VGPRs)
+#define SVH_CASE(SMV) \
+    case SMV: return reinterpret_cast<const void*>(&chain_viterbi_kernel<SMV, W, HA, false>);
+        SVH_CASE(1) SVH_CASE(2) SVH_CASE(3) SVH_CASE(4) SVH_CASE(5)
 #undef SVH_CASE
         default: return nullptr;
     }
 }
 template <int HA>
-const void* chain_ptr(int sm, int waves) {
+const void* chain_ptr(int sm, int waves, bool ge) {
     switch (waves) {
-        case 1: return chain_ptr_w<1, HA>(sm);
-        case 2: return chain_ptr_w<2, HA>(sm);
-        case 4: return chain_ptr_w<4, HA>(sm);
-        case 8: return chain_ptr_w<8, HA>(sm);
+        case 1: return chain_ptr_w<1, HA>(sm, ge);
+        case 2: return chain_ptr_w<2, HA>(sm, ge);
+        case 4: return chain_ptr_w<4, HA>(sm, ge);
+        case 8: return chain_ptr_w<8, HA>(sm, ge);
         default: return nullptr;
     }
 }
-const void* chain_fn(int sm, int waves, int ha) {
-    return ha == 1 ? chain_ptr<1>(sm, waves) : ha == 2 ? chain_ptr<2>(sm, waves) : nullptr;
+const void* chain_fn(int sm, int waves, int ha, bool ge) {
+    return ha == 1 ? chain_ptr<1>(sm, waves, ge) : ha == 2 ? chain_ptr<2>(sm, waves, ge) : nullptr;
 }
 
 }  // namespace
 
-bool chain_supported(int sm, int waves, int ha) { return chain_fn(sm, waves, ha) != nullptr; }
+bool chain_supported(int sm, int waves, int ha, bool ge) { return chain_fn(sm, waves, ha, ge) != nullptr; }
 
 hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStream_t stream) {
     const int waves = (int)(m.B / 64);
-    const void* fn = chain_fn((int)m.SM, waves, ha);
-    if ((m.dbg & 4u) && m.SM == 5 && waves == 8 && ha == 1)
-        fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, true>);
-    if ((m.dbg & 4u) && m.SM == 5 && waves == 1 && ha == 1)
-        fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 1, 1, true>);
-    if (!fn || m.B % 64 || m.S > (uint32_t)kChainMaxSym || m.erow < m.SM * m.B + kBandTail)
+    const bool ge = m.ge != 0;
+    const void* fn = chain_fn((int)m.SM, waves, ha, ge);
+    if ((m.dbg & 4u) && ha == 1) {  // diagnostic stamp builds
+        if (!ge && m.SM == 5 && waves == 8) fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, true>);
+        if (!ge && m.SM == 5 && waves == 1) fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 1, 1, false, true>);
+        if (ge && m.SM == 10 && waves == 4) fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<10, 4, 1, true, true>);
+    }
+    if (!fn || m.B % 64 || m.S > (uint32_t)kChainMaxSym || m.erow < m.SM * m.B + kBandTail ||
+        (ge && !m.erows_t))
         return hipErrorInvalidValue;
     if (b.nseq == 0) return hipSuccess;
     BandModel mm = m;

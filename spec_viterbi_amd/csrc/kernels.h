@@ -80,6 +80,7 @@ static_assert(kBandTailE + kBandHeavy <= kBandTail, "band row tail");
 
 struct BandModel {
     const float* erows;     // [S][erow]: [s*B + t] = E[o][row of position t*SM+s] (+inf pad), tail
+    const float* erows_t;   // chain kernel, streamed E: [S][B][round_up(SM,4)] (+inf pad)
     const float* start;     // [SM*B] start of light positions (+inf pad)
     const float* aw;        // [HA][SM*B] weight of the term from heavy row h
     const float* bw;        // [SM*B] weight of the term from position p-1
@@ -88,8 +89,10 @@ struct BandModel {
     int hvalid[kBandHeavy];
     float hstart[kBandHeavy];
     uint32_t n, S, B, SM, erow, H;
+    uint32_t ge;  // chain kernel: 1 = emission rows streamed from L2 (erows_t), 0 = held in VGPRs
     uint32_t dbg;  // diagnostic ablations (timing only, wrong results): 1 no DMA, 2 no barrier,
-                   // 4 s_memtime segment stamps into `stamps` (SM=5 HA=1 build only)
+                   // 4 s_memtime segment stamps into `stamps`, 8 no s_sleep in spins,
+                   // 16 chain kernel ignores the exchange tags (never waits)
     unsigned long long* stamps;  // [nseq][kMaxWaves][kBandStamps] cycle sums (dbg & 4)
     uint32_t* fault;             // chain kernel: set non-zero if a bounded spin gave up
 };
@@ -104,8 +107,8 @@ inline size_t chain_lds_bytes() {
     return (size_t)kChainMaxSym * kBandTail * sizeof(float) + 4 * 2 * kMaxWaves * 8 +
            2 * kMaxWaves * sizeof(float) + kChainSymChunk;
 }
-// Chain kernel for (SM slots, W waves, HA heavy feeders); false if not instantiated.
-bool chain_supported(int sm, int waves, int ha);
+// Chain kernel for (SM slots, W waves, HA heavy feeders, E streamed?); false if not instantiated.
+bool chain_supported(int sm, int waves, int ha, bool ge);
 hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStream_t stream);
 
 // CSR of T^T used by the generic kernel and the _spec precompute.

@@ -406,13 +406,23 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
     }
 
     uint32_t SM = 0, B = 0;
-    if (chain) {
+    bool ge = false;
+    const char* ge_env = chain ? std::getenv("SVH_CHAIN_GE") : nullptr;  // diagnostic: waves
+    if (ge_env && std::atoi(ge_env) > 0) {
+        const uint32_t w = (uint32_t)std::atoi(ge_env);
+        const uint32_t sm = (nL + 64 * w - 1) / (64 * w);
+        if (chain_supported((int)sm, (int)w, (int)std::max<uint32_t>(HA, 1), true)) {
+            SM = sm;
+            B = 64 * w;
+            ge = true;
+        }
+    } else if (chain) {
         // barrier-free kernel: fewest waves (1, 2, 4, 8) holding <= 5 positions per thread
         for (uint32_t w = 1; w <= 8 && SM == 0; w *= 2) {
             if (64 * w > (uint32_t)max_threads) break;
             const uint32_t sm = (nL + 64 * w - 1) / (64 * w);
             if (sm <= 5 || w == 8 || 128 * w > (uint32_t)max_threads) {
-                if (chain_supported((int)sm, (int)w, (int)std::max<uint32_t>(HA, 1))) {
+                if (chain_supported((int)sm, (int)w, (int)std::max<uint32_t>(HA, 1), false)) {
                     SM = sm;
                     B = 64 * w;
                 }
@@ -437,6 +447,7 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
 
     bp.ok = true;
     bp.chain = chain;
+    bp.ge = ge;
     bp.B = B;
     bp.SM = SM;
     bp.HA = HA;
@@ -462,6 +473,14 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
         bp.start[x] = hm.start[light[p]];
         bp.bw[x] = bwp[p];
         for (uint32_t a = 0; a < HA; ++a) bp.aw[(size_t)a * cap + x] = awp[order[a]][p];
+    }
+    // streamed-E chain kernel: [o][t][round_up(SM,4)]
+    if (ge) {
+        const uint32_t smp = (SM + 3) / 4 * 4;
+        bp.erows_t.assign((size_t)S * B * smp, kInfH);
+        for (uint32_t o = 0; o < S; ++o)
+            for (uint32_t p = 0; p < nL; ++p)
+                bp.erows_t[((size_t)o * B + p / SM) * smp + p % SM] = hm.emis[(size_t)o * n + light[p]];
     }
     // emission rows: permuted light part, then the folded heavy constants
     bp.erows.assign((size_t)S * erow, kInfH);
@@ -489,12 +508,15 @@ void DeviceBandPlan::upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream
     d_aw.upload(p.aw.data(), p.aw.size() * 4, s);
     d_bw.upload(p.bw.data(), p.bw.size() * 4, s);
     d_lrow.upload(p.lrow.data(), p.lrow.size() * 4, s);
+    if (p.ge) d_erows_t.upload(p.erows_t.data(), p.erows_t.size() * 4, s);
     std::memset(&view, 0, sizeof(view));
     view.erows = d_erows.as<float>();
     view.start = d_start.as<float>();
     view.aw = d_aw.as<float>();
     view.bw = d_bw.as<float>();
     view.lrow = d_lrow.as<uint32_t>();
+    view.erows_t = p.ge ? d_erows_t.as<float>() : nullptr;
+    view.ge = p.ge ? 1u : 0u;
     for (int h = 0; h < kBandHeavy; ++h) {
         view.hrow[h] = p.hrow[h];
         view.hvalid[h] = p.hvalid[h];

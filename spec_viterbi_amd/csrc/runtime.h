@@ -98,11 +98,12 @@ struct DevicePlan {
 struct BandPlan {
     bool ok = false;
     bool chain = false;  // barrier-free register kernel (chain.hip) instead of band.hip
+    bool ge = false;     // chain kernel streams E rows from L2 (erows_t) instead of VGPRs
     uint32_t B = 0, SM = 0, HA = 0, H = 0, nL = 0, erow = 0;
     int hrow[kBandHeavy] = {0, 0};
     int hvalid[kBandHeavy] = {0, 0};
     float hstart[kBandHeavy] = {0, 0};
-    std::vector<float> erows, start, aw, bw;
+    std::vector<float> erows, erows_t, start, aw, bw;
     std::vector<uint32_t> lrow;
     size_t lds_bytes = 0;
 };
@@ -110,7 +111,7 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain);
 
 struct DeviceBandPlan {
     BandPlan plan;
-    DeviceBuffer d_erows, d_start, d_aw, d_bw, d_lrow, d_stamps, d_fault;
+    DeviceBuffer d_erows, d_erows_t, d_start, d_aw, d_bw, d_lrow, d_stamps, d_fault;
     BandModel view{};
     void upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream_t s);
     void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_BAND_DEBUG & 4)
