@@ -69,18 +69,32 @@ __device__ __forceinline__ uint64_t lds_load64(const uint64_t* p) {
 __device__ __forceinline__ uint64_t pack(uint32_t tag, float v) {
     return ((uint64_t)tag << 32) | __builtin_bit_cast(uint32_t, v);
 }
-// Lane 63 alone stores both words (EXEC narrowed inside the asm and restored), so the publish
-// neither branches divergently (which would turn the loop counters into VGPRs) nor spends LDS
-// bandwidth on 63 idle lanes.
-__device__ __forceinline__ void publish_lane63(uint32_t addr, uint64_t lo, uint64_t hi) {
+// Order-preserving float key (uint order == float order, -0 < +0), and its inverse.
+__device__ __forceinline__ uint32_t fkey(float v) {
+    const uint32_t b = __builtin_bit_cast(uint32_t, v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float funkey(uint32_t k) {
+    return __builtin_bit_cast(float, (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+// Lane 63 alone publishes (EXEC narrowed inside the asm and restored), so the publish neither
+// branches divergently (which would turn the loop counters into VGPRs) nor spends LDS bandwidth
+// on 63 idle lanes:  ds_max_u64 of {tag, ~key(partial)} into the observation's min cell (larger
+// tag wins; within a tag the smallest key), then ds_add_u32 of 1 into its arrival count (LDS
+// executes one wave's operations in order, so a reader that sees the count sees the max), then
+// the tagged last score.
+__device__ __forceinline__ void publish_lane63(uint32_t cell, uint64_t cellv, uint32_t cnt,
+                                               uint32_t bnd, uint64_t bndv) {
     uint64_t saved;
     asm volatile(
-        "s_and_saveexec_b64 %0, %4\n\t"
+        "s_and_saveexec_b64 %0, %6\n\t"
         "s_nop 1\n\t"
-        "ds_write2_b64 %1, %2, %3 offset1:1\n\t"
+        "ds_max_u64 %1, %2\n\t"
+        "ds_add_u32 %3, %7\n\t"
+        "ds_write_b64 %4, %5\n\t"
         "s_mov_b64 exec, %0"
         : "=&s"(saved)
-        : "v"(addr), "v"(lo), "v"(hi), "s"(0x8000000000000000ull)
+        : "v"(cell), "v"(cellv), "v"(cnt), "v"(bnd), "v"(bndv), "s"(0x8000000000000000ull), "v"(1u)
         : "memory", "scc");
 }
 
@@ -107,7 +121,9 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     //      tagged words) | red | symbols [kChainSymChunk]
     float* ctab = lds;
     uint64_t* rec = reinterpret_cast<uint64_t*>(lds + kChainMaxSym * kBandTail);  // [kRing][kMaxWaves][2]
-    float* red = reinterpret_cast<float*>(rec + 2 * kRing * kMaxWaves);
+    uint64_t* pcell = rec + 2 * kRing * kMaxWaves;                                 // [kRing]
+    uint32_t* pcnt = reinterpret_cast<uint32_t*>(pcell + kRing);                   // [kRing] (+pad)
+    float* red = reinterpret_cast<float*>(pcnt + 2 * kRing);
     uint8_t* symr = reinterpret_cast<uint8_t*>(red + 2 * kMaxWaves);
 
     // ---- resident tables ---------------------------------------------------------------------
@@ -155,7 +171,7 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     }
     for (uint32_t x = t; x < S * kBandTail; x += B)
         ctab[x] = m.erows[(size_t)(x / kBandTail) * erow + tail + x % kBandTail];
-    for (uint32_t x = t; x < 2 * kRing * kMaxWaves; x += B) rec[x] = 0ull;
+    for (uint32_t x = t; x < 2 * kRing * kMaxWaves + kRing + kRing; x += B) rec[x] = 0ull;  // rec, cells, counts
 
     // ---- sequence ----------------------------------------------------------------------------
     const uint8_t* sym = b.symbols + b.sym_off[q];
@@ -210,55 +226,43 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         for (int s = 1; s < SM; ++s) pm = fminf(pm, vv[s]);
         return wave_min63(pm);
     };
-    // rec[k % kRing][wave] = {partial of observation k, k+1 | last score of the wave at k, k+1}:
-    // the partial is read by every wave at k+2, the last score by wave+1 at k+1.
-    // Ring slots are passed as values the group loop knows at compile time (i % 4), so record
-    // addresses are constant offsets from two per-wave bases: no scalar address work per step.
-    uint64_t* const rec_w = rec + 2 * wave;                     // this wave's column
+    // Exchange per observation k (slot = k % kRing, a compile-time constant in the group loop):
+    //   pcell[slot] = max over waves of {k+1, ~key(partial)} -> the min of the light scores of k,
+    //   pcnt[slot]  = arrivals (monotonic: W per use of the slot), read by every wave at k+2;
+    //   rec[slot][wave].hi = {last score of the wave at k, k+1}, read by wave+1 at k+1.
     const uint64_t* const rec_l = rec + 2 * (wave ? wave - 1 : 0) + 1;  // left neighbour's last scores
     auto publish = [&](uint32_t obs, uint32_t slot, float partial, float vlast) {
-        publish_lane63(lds_addr(rec_w + 2 * kMaxWaves * slot), pack(obs + 1u, partial), pack(obs + 1u, vlast));
+        publish_lane63(lds_addr(pcell + slot), ((uint64_t)(obs + 1u) << 32) | (uint64_t)(~fkey(partial)),
+                       lds_addr(pcnt + slot), lds_addr(rec + 2 * (slot * kMaxWaves + wave) + 1),
+                       pack(obs + 1u, vlast));
     };
+    // Arrivals the count of obs's slot has once every wave published obs (obs >= first - 1).
+    auto arrivals = [&](uint32_t obs) -> uint32_t { return (uint32_t)W * (((obs + 1u - first) >> 2) + 1u); };
     // Bounded spins: `spins` is wave-uniform (every decision goes through readfirstlane).
     uint32_t spins = 0;
-    // min over every wave's partial of observation obs; `w` holds a first read of the words.
-    // Fast path: the first read is current (no loop, no copies of w); slow path: re-read loop.
-    auto reduce_words = [&](const uint64_t (&w)[W], uint32_t& tmin) -> float {
-        tmin = 0xFFFFFFFFu;
-        float mu = kInf;
-#pragma unroll
-        for (int x = 0; x < W; ++x) {
-            tmin = min(tmin, (uint32_t)(w[x] >> 32));
-            mu = fminf(mu, __builtin_bit_cast(float, (uint32_t)w[x]));
-        }
-        return mu;
-    };
-    auto take_mu = [&](uint32_t obs, uint32_t slot, const uint64_t (&w0)[W]) -> float {
-        uint32_t tmin;
-        float mu = reduce_words(w0, tmin);
-        if (__builtin_expect(uniform((int)tmin) != (int)(obs + 1u), 0) && !(m.dbg & 16u)) {
-            const uint64_t* pw = rec + 2 * kMaxWaves * slot;
+    // min of the light scores of observation obs; (cnt, cell) hold a first read.
+    auto take_mu = [&](uint32_t obs, uint32_t slot, uint32_t cnt, uint64_t cell) -> float {
+        const uint32_t want = arrivals(obs);
+        if (__builtin_expect((uint32_t)uniform((int)cnt) < want, 0)) {
             while (true) {
                 if (++spins > kSpinLimit) break;
-                if (!(m.dbg & 8u)) __builtin_amdgcn_s_sleep(1);
-                uint64_t w[W];
-#pragma unroll
-                for (int x = 0; x < W; ++x) w[x] = lds_load64(pw + 2 * x);
-                mu = reduce_words(w, tmin);
-                if (uniform((int)tmin) == (int)(obs + 1u)) break;
+                __builtin_amdgcn_s_sleep(1);
+                cnt = __hip_atomic_load(pcnt + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                cell = lds_load64(pcell + slot);
+                if ((uint32_t)uniform((int)cnt) >= want) break;
             }
         }
-        return mu;
+        return funkey(~(uint32_t)cell);
     };
     // the left neighbour's last score of observation obs; `w0` holds a first read of the word
     auto take_bnd = [&](uint32_t obs, uint32_t slot, uint64_t w0) -> float {
         if (W == 1 || wave == 0) return kInf;
         uint64_t w = w0;
-        if (__builtin_expect(uniform((int)(uint32_t)(w >> 32)) != (int)(obs + 1u), 0) && !(m.dbg & 16u)) {
+        if (__builtin_expect(uniform((int)(uint32_t)(w >> 32)) != (int)(obs + 1u), 0)) {
             const uint64_t* bp = rec_l + 2 * kMaxWaves * slot;
             while (true) {
                 if (++spins > kSpinLimit) break;
-                if (!(m.dbg & 8u)) __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(1);
                 w = lds_load64(bp);
                 if (uniform((int)(uint32_t)(w >> 32)) == (int)(obs + 1u)) break;
             }
@@ -299,11 +303,11 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
                     const HeavyConst& hc_prev) -> HeavyConst {
         mark(0);
         const uint32_t s0 = k3 & (kRing - 1), s1 = (k3 + kRing - 1) & (kRing - 1), s2 = (k3 + kRing - 2) & (kRing - 1);
-        uint64_t pwv[W];
-        if (W > 1 && lagged) {
-            const uint64_t* pw = rec + 2 * kMaxWaves * s2;
-#pragma unroll
-            for (int x = 0; x < W; ++x) pwv[x] = lds_load64(pw + 2 * x);
+        uint32_t pcv = 0;
+        uint64_t pmv = 0;
+        if (W > 1 && lagged) {  // count first, then the cell (LDS keeps the order)
+            pcv = __hip_atomic_load(pcnt + s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            pmv = lds_load64(pcell + s2);
         }
         uint64_t bwv = 0;  // wave 0 has no left neighbour: no load (a dead load still costs a wait)
         if (W > 1 && wave) bwv = lds_load64(rec_l + 2 * kMaxWaves * s1);
@@ -321,11 +325,14 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         pin(xb);
         pin(xa[0]);
         if constexpr (W > 1) {
-            if (lagged) pin_u64(pwv);
+            if (lagged) {
+                pin_u64(pmv);
+                asm volatile("" : "+v"(pcv));
+            }
             pin_u64(bwv);
         }
         mark(1);
-        if (lagged) heavy_update(W > 1 ? take_mu(i - 2, s2, pwv) : own_p2, hc_prev);  // heavy scores of i-1
+        if (lagged) heavy_update(W > 1 ? take_mu(i - 2, s2, pcv, pmv) : own_p2, hc_prev);  // heavy scores of i-1
         mark(2);
         float vn[SM];
 #pragma unroll
@@ -412,13 +419,13 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         hc = step(i, i & 3u, i > first, o, e, hc);
     }
     if (len > first) {  // heavy scores of the last observation (partials of len-2)
-        const uint64_t* pw = rec + 2 * kMaxWaves * ((len - 2) & (kRing - 1));
-        uint64_t pwv[W];
+        const uint32_t sl = (len - 2) & (kRing - 1);
+        float mu = own_p2;
         if constexpr (W > 1) {
-#pragma unroll
-            for (int x = 0; x < W; ++x) pwv[x] = lds_load64(pw + 2 * x);
+            const uint32_t c = __hip_atomic_load(pcnt + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            mu = take_mu(len - 2, sl, c, lds_load64(pcell + sl));
         }
-        heavy_update(W > 1 ? take_mu(len - 2, (len - 2) & (kRing - 1), pwv) : own_p2, hc);
+        heavy_update(mu, hc);
     }
 
     if constexpr (STAMP) {

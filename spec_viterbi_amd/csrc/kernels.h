@@ -104,7 +104,7 @@ constexpr int kChainMaxSym = 32;
 constexpr int kChainMaxThreads = 512;
 constexpr uint32_t kChainSymChunk = 32768;  // symbols staged in LDS per refill
 inline size_t chain_lds_bytes() {
-    return (size_t)kChainMaxSym * kBandTail * sizeof(float) + 4 * 2 * kMaxWaves * 8 +
+    return (size_t)kChainMaxSym * kBandTail * sizeof(float) + 4 * 2 * kMaxWaves * 8 + 4 * 8 + 8 * 4 +
            2 * kMaxWaves * sizeof(float) + kChainSymChunk;
 }
 // Chain kernel for (SM slots, W waves, HA heavy feeders, E streamed?); false if not instantiated.
