@@ -19,6 +19,8 @@
 //     slack and the waves drift freely by up to two observations.
 //   * Rings of 4 tagged words per wave make overwrites safe: a wave at observation i has seen
 //     every wave finish observation i-2.  Every spin is bounded (fault word on give-up).
+#include <type_traits>
+
 #include "device_common.h"
 #include "kernels.h"
 
@@ -30,7 +32,7 @@ namespace {
 
 typedef float f32x32 __attribute__((ext_vector_type(32)));
 
-constexpr uint32_t kRing = 4;  // see the ring argument in the step comments
+constexpr uint32_t kRing = kChainRing;  // see the ring argument at the exchange
 constexpr uint32_t kSpinLimit = 1u << 22;
 
 // Empty asm that consumes the values: everything computing them is emitted before it (and a
@@ -69,33 +71,46 @@ __device__ __forceinline__ uint64_t lds_load64(const uint64_t* p) {
 __device__ __forceinline__ uint64_t pack(uint32_t tag, float v) {
     return ((uint64_t)tag << 32) | __builtin_bit_cast(uint32_t, v);
 }
-// Order-preserving float key (uint order == float order, -0 < +0), and its inverse.
-__device__ __forceinline__ uint32_t fkey(float v) {
-    const uint32_t b = __builtin_bit_cast(uint32_t, v);
-    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
-__device__ __forceinline__ float funkey(uint32_t k) {
-    return __builtin_bit_cast(float, (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
-}
-// Lane 63 alone publishes (EXEC narrowed inside the asm and restored), so the publish neither
+// The last lane of every row (15, 31, 47, 63; each holds its row's minimum after four DPP
+// stages) publishes, with EXEC narrowed inside the asm and restored, so the publish neither
 // branches divergently (which would turn the loop counters into VGPRs) nor spends LDS bandwidth
-// on 63 idle lanes:  ds_max_u64 of {tag, ~key(partial)} into the observation's min cell (larger
-// tag wins; within a tag the smallest key), then ds_add_u32 of 1 into its arrival count (LDS
-// executes one wave's operations in order, so a reader that sees the count sees the max), then
-// the tagged last score.
-__device__ __forceinline__ void publish_lane63(uint32_t cell, uint64_t cellv, uint32_t cnt,
-                                               uint32_t bnd, uint64_t bndv) {
+// on idle lanes.  In LDS order (one wave's LDS operations execute in order):
+//   ds_write_b32 +inf  -> the cell two observations ahead (wave 0; other waves hit a junk word)
+//   ds_min_f32 row min -> this observation's cell
+//   ds_add_u32 1       -> this observation's arrival count (a reader that sees every arrival
+//                         sees every row's min)
+//   ds_write_b64       -> lane 63's tagged last score (lanes 15/31/47: the unused low word)
+// Offsets are immediates: the ring slot is a template constant.
+template <uint32_t RST_OFF, uint32_t CELL_OFF, uint32_t CNT_OFF, uint32_t BND_OFF>
+__device__ __forceinline__ void publish_rows(uint32_t rbase, uint32_t cbase, float rowmin, uint32_t bbase,
+                                             uint64_t bndv, float inf, uint32_t one) {
     uint64_t saved;
     asm volatile(
         "s_and_saveexec_b64 %0, %6\n\t"
         "s_nop 1\n\t"
-        "ds_max_u64 %1, %2\n\t"
-        "ds_add_u32 %3, %7\n\t"
-        "ds_write_b64 %4, %5\n\t"
+        "ds_write_b32 %1, %7 offset:%9\n\t"
+        "ds_min_f32 %2, %3 offset:%10\n\t"
+        "ds_add_u32 %2, %8 offset:%11\n\t"
+        "ds_write_b64 %4, %5 offset:%12\n\t"
         "s_mov_b64 exec, %0"
         : "=&s"(saved)
-        : "v"(cell), "v"(cellv), "v"(cnt), "v"(bnd), "v"(bndv), "s"(0x8000000000000000ull), "v"(1u)
+        : "v"(rbase), "v"(cbase), "v"(rowmin), "v"(bbase), "v"(bndv), "s"(0x8000800080008000ull), "v"(inf),
+          "v"(one), "n"(RST_OFF), "n"(CELL_OFF), "n"(CNT_OFF), "n"(BND_OFF)
         : "memory", "scc");
+}
+
+// Row minimum in every lane of a row of 16 (quad swaps, half-row and row mirrors).
+__device__ __forceinline__ float row_min16(float x) {
+    asm("s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf"
+        : "+v"(x));
+    return x;
 }
 
 __device__ __forceinline__ unsigned long long stamp() {
@@ -117,13 +132,14 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     const uint32_t wave = (uint32_t)uniform((int)(t >> 6));
     constexpr uint32_t tail = SM * B;
 
-    // LDS: heavy constants [kChainMaxSym][kBandTail] | part[kRing][kMaxWaves] | bnd[..] (8 B
-    //      tagged words) | red | symbols [kChainSymChunk]
+    // LDS: heavy constants [kChainMaxSym][kBandTail] | rec [kRing][kMaxWaves][2] (tagged 8 B
+    //      words) | cell, count, junk [kRing] | red | symbols [kChainSymChunk] (chain_lds_bytes)
     float* ctab = lds;
-    uint64_t* rec = reinterpret_cast<uint64_t*>(lds + kChainMaxSym * kBandTail);  // [kRing][kMaxWaves][2]
-    uint64_t* pcell = rec + 2 * kRing * kMaxWaves;                                 // [kRing]
-    uint32_t* pcnt = reinterpret_cast<uint32_t*>(pcell + kRing);                   // [kRing] (+pad)
-    float* red = reinterpret_cast<float*>(pcnt + 2 * kRing);
+    uint64_t* rec = reinterpret_cast<uint64_t*>(lds + kChainMaxSym * kBandTail);
+    float* pcell = reinterpret_cast<float*>(rec + 2 * kRing * kMaxWaves);
+    uint32_t* pcnt = reinterpret_cast<uint32_t*>(pcell + kRing);
+    float* junk = reinterpret_cast<float*>(pcnt + kRing);
+    float* red = junk + kRing;
     uint8_t* symr = reinterpret_cast<uint8_t*>(red + 2 * kMaxWaves);
 
     // ---- resident tables ---------------------------------------------------------------------
@@ -171,7 +187,11 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     }
     for (uint32_t x = t; x < S * kBandTail; x += B)
         ctab[x] = m.erows[(size_t)(x / kBandTail) * erow + tail + x % kBandTail];
-    for (uint32_t x = t; x < 2 * kRing * kMaxWaves + kRing + kRing; x += B) rec[x] = 0ull;  // rec, cells, counts
+    for (uint32_t x = t; x < 2 * kRing * kMaxWaves; x += B) rec[x] = 0ull;  // tag 0: never written
+    if (t < kRing) {
+        pcell[t] = kInf;
+        pcnt[t] = 0;
+    }
 
     // ---- sequence ----------------------------------------------------------------------------
     const uint8_t* sym = b.symbols + b.sym_off[q];
@@ -226,37 +246,56 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         for (int s = 1; s < SM; ++s) pm = fminf(pm, vv[s]);
         return wave_min63(pm);
     };
-    // Exchange per observation k (slot = k % kRing, a compile-time constant in the group loop):
-    //   pcell[slot] = max over waves of {k+1, ~key(partial)} -> the min of the light scores of k,
-    //   pcnt[slot]  = arrivals (monotonic: W per use of the slot), read by every wave at k+2;
+    // Exchange per observation k (slot = k % kRing, a template constant in the group loop):
+    //   pcell[slot] = min over the rows of every wave (ds_min_f32) -> the min of the light scores
+    //                 of k, read by every wave at k+2;
+    //   pcnt[slot]  = 4W arrivals per use of the slot (monotonic) say all rows published;
     //   rec[slot][wave].hi = {last score of the wave at k, k+1}, read by wave+1 at k+1.
-    const uint64_t* const rec_l = rec + 2 * (wave ? wave - 1 : 0) + 1;  // left neighbour's last scores
-    auto publish = [&](uint32_t obs, uint32_t slot, float partial, float vlast) {
-        publish_lane63(lds_addr(pcell + slot), ((uint64_t)(obs + 1u) << 32) | (uint64_t)(~fkey(partial)),
-                       lds_addr(pcnt + slot), lds_addr(rec + 2 * (slot * kMaxWaves + wave) + 1),
-                       pack(obs + 1u, vlast));
+    // Ring argument (kRing = 8): wave 0 resets cell(k+2) to +inf in its publish of k.  The
+    // cell's previous observation k-6 was last read at k-4, and wave 0 publishing k has waited
+    // for every wave's publish of k-2 (so they all passed k-4); any wave publishing k+2 has
+    // waited for wave 0's publish of k, which LDS executes after the reset.  Tagged records are
+    // overwritten two uses after their reader waited on them.  Scores never go denormal (they are
+    // sums of -log2 probabilities), so the LDS float min equals fminf up to the sign of zero.
+    const uint64_t* const rec_l = rec + 2 * (wave ? wave - 1 : 0) + 1;  // left neighbour (wave 0: itself)
+    uint32_t cbase = lds_addr(pcell), rbase = lds_addr(wave ? junk : pcell), one = 1;
+    float inf_v = kInf;
+    asm volatile("" : "+v"(cbase), "+v"(rbase), "+v"(one), "+v"(inf_v));  // VGPR-resident operands
+    const uint32_t bbase = lds_addr(rec + 2 * wave + (lane == 63 ? 1 : 0));
+    constexpr uint32_t kCntOff = kRing * 4;
+    auto row_partial = [&](const float* vv) -> float {
+        float pm = vv[0];
+#pragma unroll
+        for (int s = 1; s < SM; ++s) pm = fminf(pm, vv[s]);
+        return row_min16(pm);
     };
-    // Arrivals the count of obs's slot has once every wave published obs (obs >= first - 1).
-    auto arrivals = [&](uint32_t obs) -> uint32_t { return (uint32_t)W * (((obs + 1u - first) >> 2) + 1u); };
+    auto publish = [&](auto slotc, uint32_t obs, float rowmin, float vlast) {
+        constexpr uint32_t K = decltype(slotc)::value;
+        publish_rows<((K + 2) % kRing) * 4, K * 4, kCntOff + K * 4, K * kMaxWaves * 16>(
+            rbase, cbase, rowmin, bbase, pack(obs + 1u, vlast), inf_v, one);
+    };
+    // Arrivals the count of obs's slot has once every row published obs (obs >= first - 1).
+    auto arrivals = [&](uint32_t obs) -> uint32_t { return 4u * W * (((obs + 1u - first) / kRing) + 1u); };
     // Bounded spins: `spins` is wave-uniform (every decision goes through readfirstlane).
     uint32_t spins = 0;
     // min of the light scores of observation obs; (cnt, cell) hold a first read.
-    auto take_mu = [&](uint32_t obs, uint32_t slot, uint32_t cnt, uint64_t cell) -> float {
+    auto take_mu = [&](uint32_t obs, uint32_t slot, uint32_t cnt, float cell) -> float {
         const uint32_t want = arrivals(obs);
         if (__builtin_expect((uint32_t)uniform((int)cnt) < want, 0)) {
             while (true) {
                 if (++spins > kSpinLimit) break;
                 __builtin_amdgcn_s_sleep(1);
                 cnt = __hip_atomic_load(pcnt + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                cell = lds_load64(pcell + slot);
+                cell = __hip_atomic_load(pcell + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if ((uint32_t)uniform((int)cnt) >= want) break;
             }
         }
-        return funkey(~(uint32_t)cell);
+        return cell;
     };
     // the left neighbour's last score of observation obs; `w0` holds a first read of the word
+    // (wave 0 reads its own word, which is always current, and takes +inf)
     auto take_bnd = [&](uint32_t obs, uint32_t slot, uint64_t w0) -> float {
-        if (W == 1 || wave == 0) return kInf;
+        if (W == 1) return kInf;
         uint64_t w = w0;
         if (__builtin_expect(uniform((int)(uint32_t)(w >> 32)) != (int)(obs + 1u), 0)) {
             const uint64_t* bp = rec_l + 2 * kMaxWaves * slot;
@@ -267,7 +306,7 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
                 if (uniform((int)(uint32_t)(w >> 32)) == (int)(obs + 1u)) break;
             }
         }
-        return __builtin_bit_cast(float, (uint32_t)w);
+        return wave ? __builtin_bit_cast(float, (uint32_t)w) : kInf;
     };
     // heavy constants of symbol o (read one observation before they are needed)
     struct HeavyConst {
@@ -299,18 +338,19 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     // the left neighbour's boundary is consumed (only lane 0's slot 0 needs it), so every exchange
     // has at least one observation of slack.  Returns the heavy constants of o.
     // k3 == i % 4 and lagged == (i > first), both compile-time constants in the group loop.
-    auto step = [&](uint32_t i, uint32_t k3, bool lagged, uint32_t o, const float (&e)[SM],
+    auto step = [&](uint32_t i, auto slotc, bool lagged, uint32_t o, const float (&e)[SM],
                     const HeavyConst& hc_prev) -> HeavyConst {
         mark(0);
-        const uint32_t s0 = k3 & (kRing - 1), s1 = (k3 + kRing - 1) & (kRing - 1), s2 = (k3 + kRing - 2) & (kRing - 1);
+        constexpr uint32_t s0 = decltype(slotc)::value, s1 = (s0 + kRing - 1) & (kRing - 1),
+                           s2 = (s0 + kRing - 2) & (kRing - 1);
         uint32_t pcv = 0;
-        uint64_t pmv = 0;
+        float pmv = 0;
         if (W > 1 && lagged) {  // count first, then the cell (LDS keeps the order)
             pcv = __hip_atomic_load(pcnt + s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            pmv = lds_load64(pcell + s2);
+            pmv = __hip_atomic_load(pcell + s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        uint64_t bwv = 0;  // wave 0 has no left neighbour: no load (a dead load still costs a wait)
-        if (W > 1 && wave) bwv = lds_load64(rec_l + 2 * kMaxWaves * s1);
+        uint64_t bwv = 0;
+        if constexpr (W > 1) bwv = lds_load64(rec_l + 2 * kMaxWaves * s1);
         const HeavyConst hc = load_heavy(o);
         // terms that do not need the heavy scores (lane 0's slot 0 is redone below)
         const float p0 = wave_shr1(v[SM - 1], kInf);
@@ -325,10 +365,7 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         pin(xb);
         pin(xa[0]);
         if constexpr (W > 1) {
-            if (lagged) {
-                pin_u64(pmv);
-                asm volatile("" : "+v"(pcv));
-            }
+            if (lagged) asm volatile("" : "+v"(pmv), "+v"(pcv));
             pin_u64(bwv);
         }
         mark(1);
@@ -351,12 +388,11 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
             for (int h = 0; h < HA; ++h) r = fminf(r, xa[h][0] + vh[h]);
             vn[0] = lane == 0 ? r : vn[0];
         }
-        const float pi = wave_partial(vn);
         if constexpr (W > 1) {
-            publish(i, s0, pi, vn[SM - 1]);
+            publish(slotc, i, row_partial(vn), vn[SM - 1]);
         } else {  // one wave: its own partials are the only ones, keep the last two in registers
             own_p2 = own_p1;
-            own_p1 = uniform_f(pi);
+            own_p1 = uniform_f(wave_partial(vn));
         }
         mark(4);
 #pragma unroll
@@ -364,51 +400,83 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         return hc;
     };
 
-    if constexpr (W > 1) publish(first - 1, (first - 1) & (kRing - 1), wave_partial(v), v[SM - 1]);
-    else own_p1 = uniform_f(wave_partial(v));
-    auto sym_word = [&](uint32_t i) -> uint32_t {  // symbols i .. i+3 (i % 4 == 0)
-        return *reinterpret_cast<const uint32_t*>(symr + (i - sbase));
+    // a call with the ring slot of obs as a template constant (head / tail of the loop)
+    auto with_slot = [&](uint32_t obs, auto&& fn) {
+        switch (obs & (kRing - 1)) {
+            case 0: return fn(std::integral_constant<uint32_t, 0>{});
+            case 1: return fn(std::integral_constant<uint32_t, 1>{});
+            case 2: return fn(std::integral_constant<uint32_t, 2>{});
+            case 3: return fn(std::integral_constant<uint32_t, 3>{});
+            case 4: return fn(std::integral_constant<uint32_t, 4>{});
+            case 5: return fn(std::integral_constant<uint32_t, 5>{});
+            case 6: return fn(std::integral_constant<uint32_t, 6>{});
+            default: return fn(std::integral_constant<uint32_t, 7>{});
+        }
     };
+    auto step_rt = [&](uint32_t i, bool lagged, uint32_t o, const float (&e)[SM], const HeavyConst& hcp) -> HeavyConst {
+        return with_slot(i, [&](auto kc) { return step(i, kc, lagged, o, e, hcp); });
+    };
+    if constexpr (W > 1) {
+        const float rm = row_partial(v);
+        with_slot(first - 1, [&](auto kc) { publish(kc, first - 1, rm, v[SM - 1]); });
+    } else {
+        own_p1 = uniform_f(wave_partial(v));
+    }
+    auto sym_dword = [&](uint32_t i) -> uint64_t {  // symbols i .. i+7 (i % 8 == 0)
+        return *reinterpret_cast<const uint64_t*>(symr + (i - sbase));
+    };
+    auto sym_of = [](uint64_t w, int k) -> uint32_t { return (uint32_t)uniform((int)((w >> (8 * k)) & 0xFFu)); };
     uint32_t i = first;
     HeavyConst hc = {};
-    // head: single steps up to a multiple of 4 (and past `first`, so group steps are lagged)
-    for (; i < len && ((i & 3u) || i == first); i = (uint32_t)uniform((int)(i + 1))) {
+    // head: single steps up to a multiple of 8 (and past `first`, so group steps are lagged)
+    for (; i < len && ((i & (kRing - 1)) || i == first); i = (uint32_t)uniform((int)(i + 1))) {
         const uint32_t o = (uint32_t)uniform((int)symr[i - sbase]);
         float e[SM];
         extract(o, e);
-        hc = step(i, i & 3u, i > first, o, e, hc);
+        hc = step_rt(i, i > first, o, e, hc);
     }
-    // body: groups of four observations, one symbol word each; GE: E rows prefetched 4 ahead
-    if (i + 4 <= len) {
-        uint32_t word = (uint32_t)uniform((int)sym_word(i));
+    // body: groups of eight observations (one ring turn), one symbol dword each; GE: E rows
+    // prefetched 4 ahead
+    if (i + kRing <= len) {
+        uint64_t word = (uint64_t)uniform((int)(uint32_t)sym_dword(i)) |
+                        ((uint64_t)(uint32_t)uniform((int)(uint32_t)(sym_dword(i) >> 32)) << 32);
         float4 eb[GE ? 4 : 1][NQ];
         if constexpr (GE) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) load_e4((word >> (8 * k)) & 0xFFu, eb[k]);
+            for (int k = 0; k < 4; ++k) load_e4(sym_of(word, k), eb[k]);
         }
-        for (; i + 4 <= len; i = (uint32_t)uniform((int)(i + 4))) {
-            if (__builtin_expect(i + 8 > sbase + kChainSymChunk, 0)) {  // uniform: refill (rare)
+        for (; i + kRing <= len; i = (uint32_t)uniform((int)(i + kRing))) {
+            if (__builtin_expect(i + 2 * kRing > sbase + kChainSymChunk, 0)) {  // uniform: refill (rare)
                 __syncthreads();  // every wave is at observation i: the old chunk is dead
                 sbase = i & ~15u;
                 stage_symbols();
                 __syncthreads();
-                word = (uint32_t)uniform((int)sym_word(i));
+                const uint64_t w2 = sym_dword(i);
+                word = (uint64_t)uniform((int)(uint32_t)w2) | ((uint64_t)(uint32_t)uniform((int)(uint32_t)(w2 >> 32)) << 32);
             }
-            const uint32_t next = sym_word(i + 4);  // zero padding past len; retired next group
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t o = (uint32_t)uniform((int)((word >> (8 * k)) & 0xFFu));
+            const uint64_t next = sym_dword(i + kRing);  // zero padding past len; retired next group
+            auto group_step = [&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                const uint32_t o = sym_of(word, k);
                 float e[SM];
                 if constexpr (GE) {
-                    e_from4(eb[k], e);
+                    e_from4(eb[k & 3], e);
                     // row of observation i+k+4 into the slot just consumed (zero padding: row 0)
-                    load_e4((uint32_t)uniform((int)((next >> (8 * k)) & 0xFFu)), eb[k]);
+                    load_e4(k < 4 ? sym_of(word, k + 4) : sym_of(next, k - 4), eb[k & 3]);
                 } else {
                     extract(o, e);
                 }
-                hc = step(i + k, (uint32_t)k, true, o, e, hc);
-            }
-            word = (uint32_t)uniform((int)next);
+                hc = step(i + k, std::integral_constant<uint32_t, (uint32_t)k>{}, true, o, e, hc);
+            };
+            group_step(std::integral_constant<int, 0>{});
+            group_step(std::integral_constant<int, 1>{});
+            group_step(std::integral_constant<int, 2>{});
+            group_step(std::integral_constant<int, 3>{});
+            group_step(std::integral_constant<int, 4>{});
+            group_step(std::integral_constant<int, 5>{});
+            group_step(std::integral_constant<int, 6>{});
+            group_step(std::integral_constant<int, 7>{});
+            word = (uint64_t)uniform((int)(uint32_t)next) | ((uint64_t)(uint32_t)uniform((int)(uint32_t)(next >> 32)) << 32);
         }
     }
     // tail
@@ -416,14 +484,14 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         const uint32_t o = (uint32_t)uniform((int)symr[i - sbase]);
         float e[SM];
         extract(o, e);
-        hc = step(i, i & 3u, i > first, o, e, hc);
+        hc = step_rt(i, i > first, o, e, hc);
     }
     if (len > first) {  // heavy scores of the last observation (partials of len-2)
         const uint32_t sl = (len - 2) & (kRing - 1);
         float mu = own_p2;
         if constexpr (W > 1) {
             const uint32_t c = __hip_atomic_load(pcnt + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            mu = take_mu(len - 2, sl, c, lds_load64(pcell + sl));
+            mu = take_mu(len - 2, sl, c, __hip_atomic_load(pcell + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         }
         heavy_update(mu, hc);
     }

@@ -103,9 +103,12 @@ constexpr int kBandStamps = 8;
 constexpr int kChainMaxSym = 32;
 constexpr int kChainMaxThreads = 512;
 constexpr uint32_t kChainSymChunk = 32768;  // symbols staged in LDS per refill
+constexpr int kChainRing = 8;  // exchange ring depth (observations in flight between waves)
 inline size_t chain_lds_bytes() {
-    return (size_t)kChainMaxSym * kBandTail * sizeof(float) + 4 * 2 * kMaxWaves * 8 + 4 * 8 + 8 * 4 +
-           2 * kMaxWaves * sizeof(float) + kChainSymChunk;
+    // heavy constants | tagged records [ring][waves][2] u64 | cells, counts, junk [ring] 4 B each |
+    // reduction | staged symbols
+    return (size_t)kChainMaxSym * kBandTail * sizeof(float) + (size_t)kChainRing * 2 * kMaxWaves * 8 +
+           3 * kChainRing * 4 + 2 * kMaxWaves * sizeof(float) + kChainSymChunk;
 }
 // Chain kernel for (SM slots, W waves, HA heavy feeders, E streamed?); false if not instantiated.
 bool chain_supported(int sm, int waves, int ha, bool ge);

@@ -1,19 +1,27 @@
-"""Multi-GPU sharding of independent observation sequences (one process per GPU).
+"""Multi-GPU sharding of independent observation sequences (one process per GPU), SURVEY.md 8(e).
 
 Sequences are independent, so a batch shards with no data-path collective: every rank holds the
-(small) HMM, runs its share, and results are gathered once at the end.  Assignment is LPT
-(longest processing time first, greedy onto the least-loaded rank) on sequence length, which
-bounds the makespan by the longest sequence plus one average share.
+(small) HMM, runs its share on its own GPU, and results are gathered once at the end (scores,
+best final states and, optionally, decoded paths).  Assignment is LPT (longest processing time
+first, greedy onto the least-loaded rank) on sequence length, which bounds the makespan by the
+longest sequence plus one average share.
+
+The gathers are all_gather of padded fixed-width tensors: RCCL has no gather, and the payloads are
+tiny (covid-19.ess: 16 x 2407 fp32 scores + 15,616 path entries), so they are latency-bound on
+xGMI whatever the collective.  The same code runs over gloo on CPU tensors (the CPU tests).
 """
 from __future__ import annotations
 
 import heapq
+import time
 
 import numpy as np
 
 
 def lpt_assign(lengths, world_size: int) -> list[list[int]]:
     """Sequence indices per rank; longest first onto the least-loaded rank (ties: lower rank)."""
+    if world_size < 1:
+        raise ValueError("world_size must be >= 1")
     order = sorted(range(len(lengths)), key=lambda q: (-int(lengths[q]), q))
     heap = [(0, r) for r in range(world_size)]
     heapq.heapify(heap)
@@ -27,38 +35,116 @@ def lpt_assign(lengths, world_size: int) -> list[list[int]]:
     return out
 
 
-def gather_scores(local_idx, local_scores: np.ndarray, nseq: int, n: int, group=None, device=None):
-    """Gather per-rank score rows to rank 0 in global sequence order (torch.distributed).
+def _gather_rows(local_idx, rows: np.ndarray, nseq: int, fill, group=None, device=None):
+    """All-gather per-rank rows [len(local_idx), width] and place them by global index on rank 0.
 
-    One gather of a padded [max_local, n] tensor plus the index lists; works over gloo (CPU
-    tensors) and nccl/RCCL (device tensors; pass `device`).  Returns the [nseq, n] array on rank
-    0 and None elsewhere.
+    Every rank pads its rows to the largest local count; one all_gather of the padded tensor plus
+    one of the index lists.  Returns [nseq, width] on rank 0, None elsewhere.
     """
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    rows = np.asarray(rows)
+    width = rows.shape[1] if rows.ndim == 2 else 1
     counts = [None] * world
-    dist.all_gather_object(counts, len(local_idx), group=group)
-    width = max(max(counts), 1)
-    buf = torch.full((width, n), float("inf"), dtype=torch.float32, device=device)
+    dist.all_gather_object(counts, (len(local_idx), list(map(int, local_idx))), group=group)
+    height = max(max(c for c, _ in counts), 1)
+    dtype = torch.from_numpy(np.zeros(0, rows.dtype)).dtype
+    buf = torch.full((height, width), fill, dtype=dtype, device=device)
     if len(local_idx):
-        buf[: len(local_idx)] = torch.as_tensor(np.asarray(local_scores, np.float32), device=device)
-    gathered = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-    if device is not None and str(device).startswith("cuda"):
-        # RCCL has no gather; all_gather moves the same bytes for this tiny payload
-        gathered = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(gathered, buf, group=group)
-    else:
-        dist.gather(buf, gathered, dst=0, group=group)
-    idx_lists = [None] * world
-    dist.all_gather_object(idx_lists, list(map(int, local_idx)), group=group)
+        buf[: len(local_idx)] = torch.from_numpy(np.ascontiguousarray(rows.reshape(len(local_idx), width))).to(buf.device)
+    gathered = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(gathered, buf, group=group)
     if rank != 0:
         return None
-    out = np.full((nseq, n), np.inf, np.float32)
+    out = np.full((nseq, width), fill, rows.dtype)
     for r in range(world):
-        rows = gathered[r].cpu().numpy()
-        for k, q in enumerate(idx_lists[r]):
-            out[q] = rows[k]
+        got = gathered[r].cpu().numpy()
+        for k, q in enumerate(counts[r][1]):
+            out[q] = got[k]
     return out
+
+
+def gather_scores(local_idx, local_scores: np.ndarray, nseq: int, n: int, group=None, device=None):
+    """Per-rank score rows [len(local_idx), n] -> [nseq, n] fp32 on rank 0 (None elsewhere)."""
+    rows = np.asarray(local_scores, np.float32).reshape(len(local_idx), n)
+    return _gather_rows(local_idx, rows, nseq, float("inf"), group, device)
+
+
+def gather_paths(local_idx, local_paths, lengths, group=None, device=None):
+    """Per-rank decoded paths (int32 arrays) -> list of nseq paths on rank 0 (None elsewhere)."""
+    width = max([int(x) for x in lengths] + [1])
+    rows = np.full((len(local_idx), width), -1, np.int32)
+    for k, p in enumerate(local_paths):
+        rows[k, : len(p)] = p
+    out = _gather_rows(local_idx, rows, len(lengths), -1, group, device)
+    if out is None:
+        return None
+    return [out[q, : int(lengths[q])].copy() for q in range(len(lengths))]
+
+
+def _hip_compute(device: int):
+    """The product's shard compute: one DeviceModel batch on this rank's GPU (fails loudly
+    without the HIP library)."""
+    from .viterbi import DeviceModel
+
+    def compute(hmm, seqs, level: int, paths: bool):
+        model = DeviceModel(hmm, device=device)
+        try:
+            if level >= 2:
+                model.spec_build(level)
+            batch = model.batch(seqs, paths=paths)
+            try:
+                batch.run(level)
+                return batch.read(want_paths=paths)
+            finally:
+                batch.close()
+        finally:
+            model.close()
+
+    return compute
+
+
+def run_sharded(hmm, seqs, *, level: int = 0, paths: bool = False, group=None, device=None,
+                compute=None):
+    """Viterbi over `seqs` sharded across the ranks of `group` (torch.distributed, initialised).
+
+    Each rank runs its LPT share with `compute(hmm, local_seqs, level, paths)` -- by default the
+    HIP DeviceModel on `device` (this rank's GPU) -- and the results are gathered to rank 0.
+    `device` is also where the gather tensors live ("cuda:k" for RCCL, None for gloo).
+    Returns (scores [nseq, n], best [nseq], paths or None, seconds_max_over_ranks) on rank 0 and
+    (None, None, None, seconds) elsewhere.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lengths = [int(np.asarray(s).size) for s in seqs]
+    mine = lpt_assign(lengths, world)[rank]
+    if compute is None:
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        compute = _hip_compute(dev.index or 0)
+    n = int(hmm.states_num)
+    dist.barrier(group)
+    t0 = time.perf_counter()
+    if mine:
+        res = compute(hmm, [seqs[q] for q in mine], level, paths)
+        scores, best = res[0], res[1]
+        local_paths = res[2] if paths else []
+    else:
+        scores = np.zeros((0, n), np.float32)
+        best = np.zeros(0, np.int64)
+        local_paths = []
+    seconds = time.perf_counter() - t0
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    seconds = float(t.item())
+    all_scores = gather_scores(mine, scores, len(seqs), n, group, device)
+    all_best = _gather_rows(mine, np.asarray(best, np.int64).reshape(-1, 1), len(seqs), -1, group, device)
+    all_paths = gather_paths(mine, local_paths, lengths, group, device) if paths else None
+    if rank != 0:
+        return None, None, None, seconds
+    return all_scores, all_best.reshape(-1), all_paths, seconds
