@@ -88,6 +88,14 @@ def _load():
         raise ImportError(
             f"{LIB_PATH} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()' "
             "or `make -j16`). There is no CPU fallback.")
+    # One HIP runtime per process, shared with PyTorch: torch's bundled libamdhip64 and ours have
+    # the same soname, so whichever loads first serves both.  Loading ours first and letting torch
+    # initialise the GPU afterwards left our hipGetDevice reporting no device (seen on MI355X), so
+    # torch, when present, loads first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

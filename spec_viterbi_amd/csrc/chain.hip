@@ -83,7 +83,7 @@ __device__ __forceinline__ uint64_t pack(uint32_t tag, float v) {
 // Offsets are immediates: the ring slot is a template constant.
 template <uint32_t RST_OFF, uint32_t CELL_OFF, uint32_t CNT_OFF, uint32_t BND_OFF>
 __device__ __forceinline__ void publish_rows(uint32_t rbase, uint32_t cbase, float rowmin, uint32_t bbase,
-                                             uint64_t bndv, float inf, uint32_t one) {
+                                             uint64_t bndv, float inf, uint32_t one, uint64_t lanes) {
     uint64_t saved;
     asm volatile(
         "s_and_saveexec_b64 %0, %6\n\t"
@@ -94,7 +94,7 @@ __device__ __forceinline__ void publish_rows(uint32_t rbase, uint32_t cbase, flo
         "ds_write_b64 %4, %5 offset:%12\n\t"
         "s_mov_b64 exec, %0"
         : "=&s"(saved)
-        : "v"(rbase), "v"(cbase), "v"(rowmin), "v"(bbase), "v"(bndv), "s"(0x8000800080008000ull), "v"(inf),
+        : "v"(rbase), "v"(cbase), "v"(rowmin), "v"(bbase), "v"(bndv), "s"(lanes), "v"(inf),
           "v"(one), "n"(RST_OFF), "n"(CELL_OFF), "n"(CNT_OFF), "n"(BND_OFF)
         : "memory", "scc");
 }
@@ -121,7 +121,7 @@ __device__ __forceinline__ unsigned long long stamp() {
     return x;
 }
 
-template <int SM, int W, int HA, bool GE, bool STAMP = false>
+template <int SM, int W, int HA, bool GE, bool STAMP = false, int DIAG = 0>
 __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
     constexpr int HM = kBandHeavy;
     constexpr uint32_t B = 64 * W;
@@ -131,6 +131,9 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     const uint32_t t = threadIdx.x, lane = t & 63u, q = blockIdx.x;
     const uint32_t wave = (uint32_t)uniform((int)(t >> 6));
     constexpr uint32_t tail = SM * B;
+    // diagnostic ablations (never planned): 1 = lane 63 alone publishes, 2 = no arrival check
+    // of the partial cells, 4 = no tag check of the boundary words (2 and 4 give wrong results)
+    constexpr bool PUB1 = DIAG & 1, NO_MU_WAIT = DIAG & 2, NO_BND_WAIT = DIAG & 4;
 
     // LDS: heavy constants [kChainMaxSym][kBandTail] | rec [kRing][kMaxWaves][2] (tagged 8 B
     //      words) | cell, count, junk [kRing] | red | symbols [kChainSymChunk] (chain_lds_bytes)
@@ -267,24 +270,25 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         float pm = vv[0];
 #pragma unroll
         for (int s = 1; s < SM; ++s) pm = fminf(pm, vv[s]);
+        if constexpr (PUB1) return wave_min63(pm);  // diagnostic: lane 63 alone publishes
         return row_min16(pm);
     };
     auto publish = [&](auto slotc, uint32_t obs, float rowmin, float vlast) {
         constexpr uint32_t K = decltype(slotc)::value;
         publish_rows<((K + 2) % kRing) * 4, K * 4, kCntOff + K * 4, K * kMaxWaves * 16>(
-            rbase, cbase, rowmin, bbase, pack(obs + 1u, vlast), inf_v, one);
+            rbase, cbase, rowmin, bbase, pack(obs + 1u, vlast), inf_v, one, PUB1 ? 0x8000000000000000ull : 0x8000800080008000ull);
     };
     // Arrivals the count of obs's slot has once every row published obs (obs >= first - 1).
-    auto arrivals = [&](uint32_t obs) -> uint32_t { return 4u * W * (((obs + 1u - first) / kRing) + 1u); };
+    auto arrivals = [&](uint32_t obs) -> uint32_t { return (PUB1 ? 1u : 4u) * W * (((obs + 1u - first) / kRing) + 1u); };
     // Bounded spins: `spins` is wave-uniform (every decision goes through readfirstlane).
-    uint32_t spins = 0;
+    uint32_t spins = 0, spins_b = 0;  // all slow-path re-reads / those of boundary words
     // min of the light scores of observation obs; (cnt, cell) hold a first read.
     auto take_mu = [&](uint32_t obs, uint32_t slot, uint32_t cnt, float cell) -> float {
         const uint32_t want = arrivals(obs);
-        if (__builtin_expect((uint32_t)uniform((int)cnt) < want, 0)) {
-            while (true) {
+        if (!NO_MU_WAIT && __builtin_expect((uint32_t)uniform((int)cnt) < want, 0)) {
+            for (uint32_t k = 0;; ++k) {
                 if (++spins > kSpinLimit) break;
-                __builtin_amdgcn_s_sleep(1);
+                if (k >= 2) __builtin_amdgcn_s_sleep(1);  // the first re-reads go straight out
                 cnt = __hip_atomic_load(pcnt + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 cell = __hip_atomic_load(pcell + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if ((uint32_t)uniform((int)cnt) >= want) break;
@@ -297,9 +301,10 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     auto take_bnd = [&](uint32_t obs, uint32_t slot, uint64_t w0) -> float {
         if (W == 1) return kInf;
         uint64_t w = w0;
-        if (__builtin_expect(uniform((int)(uint32_t)(w >> 32)) != (int)(obs + 1u), 0)) {
+        if (!NO_BND_WAIT && __builtin_expect(uniform((int)(uint32_t)(w >> 32)) != (int)(obs + 1u), 0)) {
             const uint64_t* bp = rec_l + 2 * kMaxWaves * slot;
             while (true) {
+                ++spins_b;
                 if (++spins > kSpinLimit) break;
                 __builtin_amdgcn_s_sleep(1);
                 w = lds_load64(bp);
@@ -333,6 +338,8 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     };
 
     float own_p1 = kInf, own_p2 = kInf;  // W == 1: partials of the last two observations
+    uint32_t pc_next = 0;                 // W > 1: count and cell of the observation before the
+    float pm_next = kInf;                 // current one, read half a step before they are needed
     // One observation i with symbol o.  hc_prev: heavy constants of the symbol of i-1.  Order:
     // everything that does not need another wave first; the wave's last score is published before
     // the left neighbour's boundary is consumed (only lane 0's slot 0 needs it), so every exchange
@@ -343,12 +350,8 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         mark(0);
         constexpr uint32_t s0 = decltype(slotc)::value, s1 = (s0 + kRing - 1) & (kRing - 1),
                            s2 = (s0 + kRing - 2) & (kRing - 1);
-        uint32_t pcv = 0;
-        float pmv = 0;
-        if (W > 1 && lagged) {  // count first, then the cell (LDS keeps the order)
-            pcv = __hip_atomic_load(pcnt + s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            pmv = __hip_atomic_load(pcell + s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        uint32_t pcv = pc_next;  // count and cell of i-2, read during step i-1
+        float pmv = pm_next;
         uint64_t bwv = 0;
         if constexpr (W > 1) bwv = lds_load64(rec_l + 2 * kMaxWaves * s1);
         const HeavyConst hc = load_heavy(o);
@@ -366,10 +369,13 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         pin(xa[0]);
         if constexpr (W > 1) {
             if (lagged) asm volatile("" : "+v"(pmv), "+v"(pcv));
-            pin_u64(bwv);
         }
         mark(1);
         if (lagged) heavy_update(W > 1 ? take_mu(i - 2, s2, pcv, pmv) : own_p2, hc_prev);  // heavy scores of i-1
+        if constexpr (W > 1) {  // count first, then the cell of i-1 for the next step (LDS keeps the order)
+            pc_next = __hip_atomic_load(pcnt + s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            pm_next = __hip_atomic_load(pcell + s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         mark(2);
         float vn[SM];
 #pragma unroll
@@ -380,6 +386,7 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
             vn[s] = r;
         }
         mark(3);
+        pin(vn);  // the light scores first: the boundary word has had the most time to land
         // lane 0, slot 0: the chain predecessor is the left neighbour's last score of i-1
         {
             const float bv = take_bnd(i - 1, s1, bwv);
@@ -489,20 +496,16 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     if (len > first) {  // heavy scores of the last observation (partials of len-2)
         const uint32_t sl = (len - 2) & (kRing - 1);
         float mu = own_p2;
-        if constexpr (W > 1) {
-            const uint32_t c = __hip_atomic_load(pcnt + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            mu = take_mu(len - 2, sl, c, __hip_atomic_load(pcell + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        }
+        if constexpr (W > 1) mu = take_mu(len - 2, sl, pc_next, pm_next);
         heavy_update(mu, hc);
     }
 
-    if constexpr (STAMP) {
-        if (lane == 0 && m.stamps) {
-            mark(5);
-            st_acc[6] = spins;
-            for (int k = 0; k < kBandStamps; ++k)
-                m.stamps[((size_t)q * kMaxWaves + wave) * kBandStamps + k] = st_acc[k];
-        }
+    if (lane == 0 && m.stamps) {  // diagnostics (SVH_BAND_DEBUG & 4: segment stamps, & 128: spins only)
+        mark(5);
+        st_acc[6] = spins;
+        st_acc[7] = spins_b;
+        for (int k = 0; k < kBandStamps; ++k)
+            m.stamps[((size_t)q * kMaxWaves + wave) * kBandStamps + k] = st_acc[k];
     }
     if (spins > kSpinLimit && lane == 0 && m.fault) atomicOr(m.fault, 1u);
 
@@ -586,6 +589,15 @@ hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStre
         if (!ge && m.SM == 5 && waves == 8) fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, true>);
         if (!ge && m.SM == 5 && waves == 1) fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 1, 1, false, true>);
         if (ge && m.SM == 10 && waves == 4) fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<10, 4, 1, true, true>);
+    }
+    if ((m.dbg & (64u | 2048u | 4096u)) && ha == 1 && !ge && m.SM == 5 && waves == 8) {  // diagnostic ablations
+        switch (((m.dbg >> 6) & 1u) | ((m.dbg >> 10) & 6u)) {
+            case 1: fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, false, 1>); break;
+            case 2: fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, false, 2>); break;
+            case 4: fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, false, 4>); break;
+            case 6: fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, false, 6>); break;
+            default: break;
+        }
     }
     if (!fn || m.B % 64 || m.S > (uint32_t)kChainMaxSym || m.erow < m.SM * m.B + kBandTail ||
         (ge && !m.erows_t))

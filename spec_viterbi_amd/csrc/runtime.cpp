@@ -418,7 +418,10 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
         }
     } else if (chain) {
         // barrier-free kernel: fewest waves (1, 2, 4, 8) holding <= 5 positions per thread
-        for (uint32_t w = 1; w <= 8 && SM == 0; w *= 2) {
+        // (SVH_CHAIN_WAVES=<w>: diagnostic override of the wave count)
+        const char* wv_env = std::getenv("SVH_CHAIN_WAVES");
+        const uint32_t w_force = wv_env ? (uint32_t)std::atoi(wv_env) : 0;
+        for (uint32_t w = w_force ? w_force : 1; w <= 8 && SM == 0; w *= 2) {
             if (64 * w > (uint32_t)max_threads) break;
             const uint32_t sm = (nL + 64 * w - 1) / (64 * w);
             if (sm <= 5 || w == 8 || 128 * w > (uint32_t)max_threads) {
@@ -533,7 +536,7 @@ void DeviceBandPlan::upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream
     view.fault = d_fault.as<uint32_t>();
     const char* dbg = std::getenv("SVH_BAND_DEBUG");  // diagnostic ablations only
     view.dbg = dbg ? (uint32_t)std::atoi(dbg) : 0u;
-    if (view.dbg & 4u) {
+    if (view.dbg & (4u | 128u)) {
         d_stamps.alloc((size_t)4096 * kMaxWaves * kBandStamps * 8);
         hip_check(hipMemsetAsync(d_stamps.ptr, 0, d_stamps.bytes, s), "stamps");
         view.stamps = d_stamps.as<unsigned long long>();
@@ -541,7 +544,7 @@ void DeviceBandPlan::upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream
 }
 
 void DeviceBandPlan::report_stamps(uint32_t nseq) const {
-    if (!(view.dbg & 4u) || !view.stamps) return;
+    if (!(view.dbg & (4u | 128u)) || !view.stamps) return;
     std::vector<unsigned long long> h((size_t)nseq * kMaxWaves * kBandStamps);
     if (hipMemcpy(h.data(), view.stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     double sum[kBandStamps] = {};
@@ -854,7 +857,7 @@ void Batch::run(uint32_t level, hipStream_t s) {
             const int ha = (int)std::max<uint32_t>(bpl->plan.HA, 1);
             if (bpl->plan.chain) hip_check(launch_chain(bpl->view, ha, b, s), "chain Viterbi kernel");
             else hip_check(launch_band(bpl->view, ha, b, s), "band Viterbi kernel");
-            if (bpl->view.dbg & 4u) {
+            if (bpl->view.dbg & (4u | 128u)) {
                 hip_check(hipStreamSynchronize(s), "stamps");
                 bpl->report_stamps(b.nseq);
             }

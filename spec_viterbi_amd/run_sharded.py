@@ -1,0 +1,65 @@
+"""Sharded Viterbi over one node's GPUs: one process per GPU, LPT sequence
+assignment, one gather of scores / best states / paths to rank 0.
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m spec_viterbi_amd.run_sharded \\
+        --model data/chmm_files/2405.chmm --ess data/ess_files/covid-19.ess --paths --out res.npz
+
+Without torchrun it runs as a single rank.  Rank 0 prints one JSON summary line (max-over-ranks
+time of the shard compute, state-updates/s) and, with --out, writes scores [nseq, n], best [nseq]
+and the concatenated paths with their offsets to an .npz file.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+
+import numpy as np
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--model", required=True)
+    p.add_argument("--ess", required=True)
+    p.add_argument("--level", type=int, default=0)
+    p.add_argument("--paths", action="store_true")
+    p.add_argument("--out", default="")
+    p.add_argument("--backend", default="", help="nccl (default with GPUs) or gloo")
+    args = p.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+
+    from . import read_emit_seq, read_HMM
+    from .sharding import run_sharded
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "RANK" not in os.environ:  # single process
+        os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29533"))
+    backend = args.backend or ("nccl" if torch.cuda.device_count() > 0 else "gloo")
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+    dist.init_process_group(backend, init_method="env://")
+    try:
+        hmm = read_HMM(args.model)
+        seqs = read_emit_seq(args.ess)
+        device = f"cuda:{local}" if backend == "nccl" else None
+        scores, best, paths, secs = run_sharded(hmm, seqs, level=args.level, paths=args.paths, device=device)
+        if dist.get_rank() == 0:
+            updates = int(hmm.states_num) * sum(int(s.size) for s in seqs)
+            print(json.dumps({"sequences": len(seqs), "states": int(hmm.states_num), "ranks": dist.get_world_size(),
+                              "seconds": round(secs, 6), "M_state_updates_per_s": round(updates / secs / 1e6, 2)}),
+                  flush=True)
+            if args.out:
+                extra = {}
+                if paths is not None:
+                    offs = np.zeros(len(paths) + 1, np.int64)
+                    offs[1:] = np.cumsum([len(x) for x in paths])
+                    extra = {"paths": np.concatenate(paths) if paths else np.zeros(0, np.int32), "path_offsets": offs}
+                np.savez(args.out, scores=scores, best=best, **extra)
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -13,6 +13,7 @@ xGMI whatever the collective.  The same code runs over gloo on CPU tensors (the 
 from __future__ import annotations
 
 import heapq
+import os
 import time
 
 import numpy as np
@@ -125,8 +126,8 @@ def run_sharded(hmm, seqs, *, level: int = 0, paths: bool = False, group=None, d
     lengths = [int(np.asarray(s).size) for s in seqs]
     mine = lpt_assign(lengths, world)[rank]
     if compute is None:
-        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        compute = _hip_compute(dev.index or 0)
+        index = torch.device(device).index if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
+        compute = _hip_compute(index or 0)
     n = int(hmm.states_num)
     dist.barrier(group)
     t0 = time.perf_counter()

@@ -3,6 +3,8 @@
 Scores must be bit-identical to GraphBLAS_impl's association (-0.0 == +0.0), best states and
 decoded paths identical (lowest index on ties).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -241,3 +243,26 @@ def test_band_rejects_non_chain_models():
         with pytest.raises(_lib.SvhError) as e:
             svh.DeviceModel(hmm, kernel=k)
         assert e.value.code == _lib.SVH_E_UNSUPPORTED
+
+
+def test_run_sharded_cli_covid_paths(tmp_path):
+    """The sharded runner as one RCCL rank on this GPU: covid-19 x 2405, scores,
+    best states and decoded paths gathered through run_sharded, checked against the oracle."""
+    import subprocess
+    import sys
+
+    out = tmp_path / "res.npz"
+    env = dict(os.environ, MASTER_PORT="29561")
+    r = subprocess.run([sys.executable, "-m", "spec_viterbi_amd.run_sharded", "--model", chmm("2405.chmm"),
+                        "--ess", ess("covid-19.ess"), "--paths", "--out", str(out)],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = np.load(out)
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("covid-19.ess"))
+    offs = res["path_offsets"]
+    for q in (0, 5, len(seqs) - 1):
+        sc, best, path = oracle.decode(hmm, seqs[q])
+        assert bit_equal(res["scores"][q], sc), first_mismatch(res["scores"][q], sc)
+        assert int(res["best"][q]) == best
+        assert np.array_equal(res["paths"][offs[q]:offs[q + 1]], path)

@@ -31,6 +31,10 @@ def main():
         kv = dict(x.split("=") for x in spec.split(","))
         os.environ["SVH_CHAIN_GE"] = kv.get("GE", "0")
         os.environ["SVH_BAND_DEBUG"] = kv.get("dbg", "0")
+        if "waves" in kv:
+            os.environ["SVH_CHAIN_WAVES"] = kv["waves"]
+        else:
+            os.environ.pop("SVH_CHAIN_WAVES", None)
         model = svh.DeviceModel(hmm, kernel=int(kv.get("kernel", "0")), max_threads=int(kv.get("threads", "0")))
         batch = model.batch(seqs)
         batch.run()
