@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 DATA = os.path.join(ROOT, "data")
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain"}
 
 
 def parse():
@@ -179,11 +180,11 @@ def main():
             "data": "2405.chmm + emit_50_3500_20.ess (reference files) on rank 0; same-shape synthetic "
                     "sequences (numpy default_rng(rank)) on ranks > 0",
             "config": {
-                "workload": f"{args.model} x {args.ess}, " + ("non-spec fused (min,+) step" if args.level <= 1
+                "workload": f"{args.model} x {args.ess}, " + (f"non-spec (min,+) step, {KERNEL_NAMES.get(info['kernel'], '?')} kernel" if args.level <= 1
                                                               else f"_spec level {args.level}"),
                 "states": n, "nnz": nnz, "sequences_per_gpu": len(seqs), "observations_per_gpu": steps_obs,
                 "state_updates_per_gpu": updates_per_rank, "level": args.level,
-                "kernel": {1: "fused", 2: "generic", 3: "band", 4: "chain"}.get(info["kernel"], "?"), "threads": info["threads"],
+                "kernel": KERNEL_NAMES.get(info["kernel"], "?"), "threads": info["threads"],
                 "slots": info["slots"], "heavy_rows": info["heavy_rows"], "heavy_uniform": info["heavy_uniform"],
                 "parallelism": f"sequence-sharded x{world} (one process per GPU, no collective)",
             },

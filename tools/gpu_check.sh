@@ -5,7 +5,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 420 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 &&
+timeout -k 10 420 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 &&
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 &&
 bash tools/profile.sh
 rc=$?
