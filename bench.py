@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-check", action="store_true", help="skip the golden check (diagnostic ablations only)")
+    p.add_argument("--paths", action="store_true", help="also decode paths (backpointers + traceback) every step")
     return p.parse_args()
 
 
@@ -49,6 +50,24 @@ def algorithmic_bytes_per_step(n: int, nnz: int) -> int:
     """streamed-CSR bytes of one observation of one sequence:
     8*nnz (value + index) + 4*(n+1) (row pointers) + 4n (emission row) + 4n (read v) + 4n (write v)."""
     return 8 * nnz + 4 * (n + 1) + 12 * n
+
+
+def algorithmic_bytes_per_launch(n: int, nnz: int, lengths, level: int, paths: bool) -> int:
+    """Bytes one launch must move under SURVEY.md 8(d)'s model, per sequence of length L:
+    level <= 1: (L-1) streamed-CSR steps (+ 2n uint16 backpointers per step and 4 B per path entry
+    with paths); level >= 2: floor((L-1)/level) dense products (4*n*round_up(n,4) + 8n each, the
+    product is read whole) plus the (L-1) % level tail steps streamed-CSR."""
+    step = algorithmic_bytes_per_step(n, nnz)
+    total = 0
+    for L in lengths:
+        if level >= 2:
+            chunks, tail = divmod(L - 1, level)
+            total += chunks * (4 * n * ((n + 3) // 4 * 4) + 8 * n) + tail * step
+        else:
+            total += (L - 1) * step
+            if paths:
+                total += (L - 1) * 2 * n * 2 + 4 * L  # backpointers written and read back, path
+    return total
 
 
 def cpu_baseline(hmm, seqs, seconds: float) -> dict:
@@ -105,9 +124,14 @@ def main():
     n = int(hmm.states_num)
     model = svh.DeviceModel(hmm, device=local, kernel=args.kernel, max_threads=args.max_threads)
     info = model.info()
-    if args.level >= 2:
+    prep_s = None
+    if args.level >= 2:  # spec_with, timed apart from the run as bench_Viterbi_spec.h:69-71 does
+        torch.cuda.synchronize()
+        t_prep = time.perf_counter()
         model.spec_build(args.level)
-    batch = model.batch(seqs)
+        torch.cuda.synchronize()
+        prep_s = time.perf_counter() - t_prep
+    batch = model.batch(seqs, paths=args.paths)
     # A stream of our own: torch's default stream has handle 0, which the C ABI reads as "the
     # model's own stream", so events recorded on torch's default stream would not bracket the
     # kernel.  Every launch and every event below goes to this one stream.
@@ -158,7 +182,7 @@ def main():
     if rank == 0:
         nnz = int(info["nnz"])
         steps_obs = sum(int(s.size) for s in seqs)
-        algo = algorithmic_bytes_per_step(n, nnz) * steps_obs  # bytes per launch (one rank)
+        algo = algorithmic_bytes_per_launch(n, nnz, [int(x.size) for x in seqs], args.level, args.paths)
         achieved = algo / (kernel_ms * 1e-3) / 1e9
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -166,7 +190,7 @@ def main():
             with open(pmc_path) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         out = {
-            "metric": "M state-updates/sec (states x obs/s) on 2405.chmm x emit_50_3500_20.ess",
+            "metric": f"M state-updates/sec (states x obs/s) on {args.model} x {args.ess}",
             "value": round(value, 2),
             "unit": "M state-updates/s",
             "n_gpus": world,
@@ -184,7 +208,8 @@ def main():
                                                               else f"_spec level {args.level}"),
                 "states": n, "nnz": nnz, "sequences_per_gpu": len(seqs), "observations_per_gpu": steps_obs,
                 "state_updates_per_gpu": updates_per_rank, "level": args.level,
-                "kernel": KERNEL_NAMES.get(info["kernel"], "?"), "threads": info["threads"],
+                "kernel": ("fused+traceback" if args.paths else KERNEL_NAMES.get(info["kernel"], "?")),
+                "paths": bool(args.paths), "spec_prep_s": None if prep_s is None else round(prep_s, 4), "threads": info["threads"],
                 "slots": info["slots"], "heavy_rows": info["heavy_rows"], "heavy_uniform": info["heavy_uniform"],
                 "parallelism": f"sequence-sharded x{world} (one process per GPU, no collective)",
             },

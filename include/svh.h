@@ -67,7 +67,9 @@ void svh_ess_free(svh_ess_t e);
 /* AUTO: for scores-only passes over chain-shaped (MSV) models the barrier-free register chain
  * kernel (CHAIN, emit_num <= 32, <= 2560 light states), else the barrier chain kernel (BAND);
  * otherwise the fused kernel, else the generic one.  BAND / CHAIN force that kernel (error if the
- * model does not qualify); path runs always use the fused (or generic) kernel. */
+ * model does not qualify).  Path runs use the chain kernel's decoded-path variant when the model
+ * is chain-shaped with at most one heavy row feeding the light rows (every reference .chmm), else
+ * the fused (or generic) kernel with 16-bit backpointers. */
 enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2, SVH_KERNEL_BAND = 3,
        SVH_KERNEL_CHAIN = 4 };
 
@@ -101,6 +103,8 @@ typedef struct {
     uint64_t lds_bytes;
     uint64_t spec_level;   /* level of the products built by svh_spec_build (0/1: none needed) */
     uint64_t spec_bytes;   /* HBM held by the products */
+    int32_t paths_kernel;  /* kernel of decoded-path runs (SVH_KERNEL_CHAIN, _FUSED or _GENERIC) */
+    int32_t reserved;
 } svh_model_info;
 int svh_model_get_info(svh_model_t m, svh_model_info* info);
 

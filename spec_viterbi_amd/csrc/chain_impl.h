@@ -1,4 +1,4 @@
-// Barrier-free chain Viterbi kernel (gfx950) for MSV-shaped models (N, M_1..M_L, C; the shape of
+// Barrier-free chain Viterbi kernel template (gfx950) for MSV-shaped models (N, M_1..M_L, C; the shape of
 // every reference .chmm, chmm_files/silent_hmm_to_chmm.py), emit_num <= 32.
 //
 // Reference hot loop: Viterbi_impl/GraphBLAS_impl.cpp:59-73 (same association, bit-identical):
@@ -19,6 +19,8 @@
 //     slack and the waves drift freely by up to two observations.
 //   * Rings of 4 tagged words per wave make overwrites safe: a wave at observation i has seen
 //     every wave finish observation i-2.  Every spin is bounded (fault word on give-up).
+#pragma once
+
 #include <type_traits>
 
 #include "device_common.h"
@@ -113,6 +115,69 @@ __device__ __forceinline__ float row_min16(float x) {
     return x;
 }
 
+// dst[L] = x (x wave-uniform, in an SGPR; the lane an inline constant: one constant-bus read)
+template <uint32_t L>
+__device__ __forceinline__ void writelane(uint32_t& dst, uint32_t x) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(x), "n"(L));
+}
+
+// f(integral_constant<int, I>) for I in [I0, N): a loop whose index is a constant expression
+template <int I, int N>
+struct StaticFor {
+    template <class F>
+    __device__ __forceinline__ static void run(F& f) {
+        f(std::integral_constant<int, I>{});
+        StaticFor<I + 1, N>::run(f);
+    }
+};
+template <int N>
+struct StaticFor<N, N> {
+    template <class F>
+    __device__ __forceinline__ static void run(F&) {}
+};
+
+// Unsigned row minimum (the lowest light row achieving a heavy row's light-set minimum).
+__device__ __forceinline__ uint32_t row_min16_u32(uint32_t x) {
+    asm("s_nop 1\n\t"
+        "v_min_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_u32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_u32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf"
+        : "+v"(x));
+    return x;
+}
+
+// publish_rows plus the decoded-path cells: wave 0 resets the two j* cells two observations
+// ahead (other waves hit junk words), every row adds its j* candidates (ds_min_u32) before the
+// arrival count, so a reader that sees every arrival of observation k sees every candidate.
+template <uint32_t RST_OFF, uint32_t CELL_OFF, uint32_t CNT_OFF, uint32_t BND_OFF, uint32_t JRST_OFF,
+          uint32_t JCELL_OFF>
+__device__ __forceinline__ void publish_rows_paths(uint32_t rbase, uint32_t cbase, float rowmin, uint32_t bbase,
+                                                   uint64_t bndv, float inf, uint32_t one, uint64_t lanes,
+                                                   uint32_t jrbase, uint32_t jcbase, uint32_t c0, uint32_t c1,
+                                                   uint64_t ones) {
+    uint64_t saved;
+    asm volatile(
+        "s_and_saveexec_b64 %0, %6\n\t"
+        "s_nop 1\n\t"
+        "ds_write_b32 %1, %7 offset:%13\n\t"
+        "ds_write_b64 %9, %12 offset:%17\n\t"
+        "ds_min_f32 %2, %3 offset:%14\n\t"
+        "ds_min_u32 %10, %11 offset:%18\n\t"
+        "ds_min_u32 %10, %19 offset:%20\n\t"
+        "ds_add_u32 %2, %8 offset:%15\n\t"
+        "ds_write_b64 %4, %5 offset:%16\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "v"(rbase), "v"(cbase), "v"(rowmin), "v"(bbase), "v"(bndv), "s"(lanes), "v"(inf), "v"(one),
+          "v"(jrbase), "v"(jcbase), "v"(c0), "v"(ones), "n"(RST_OFF), "n"(CELL_OFF), "n"(CNT_OFF),
+          "n"(BND_OFF), "n"(JRST_OFF), "n"(JCELL_OFF), "v"(c1), "n"(JCELL_OFF + 4)
+        : "memory", "scc");
+}
+
 __device__ __forceinline__ unsigned long long stamp() {
     unsigned long long x;
     __builtin_amdgcn_sched_barrier(0);
@@ -121,8 +186,19 @@ __device__ __forceinline__ unsigned long long stamp() {
     return x;
 }
 
-template <int SM, int W, int HA, bool GE, bool STAMP = false, int DIAG = 0>
+// PATHS (decoded paths; HA <= 1, every sequence starts at step 0) adds the backpointers of every
+// observation, in the order of the oracle's lexicographic (value, row) argmin:
+//   * light position p: its two candidates (position p-1, heavy row 0) are compared in every lane
+//     and one 64-bit lane mask per slot records "took the heavy term" (staged in a VGPR by
+//     v_writelane, stored every four observations);
+//   * heavy row h: the heavy-term argmin and the flag heavy / light / tie / none are decided where
+//     the heavy scores are (every thread, redundantly; wave 0 stores them).  The light-set argmin
+//     j* = the lowest light row with fl(c + v[j]) == fl(c + min v) is a second pass over the
+//     light scores once the minimum is known: two observations later, over a kept copy of the
+//     scores, reduced through two more LDS min cells published before the arrival count.
+template <int SM, int W, int HA, bool GE, bool STAMP = false, int DIAG = 0, bool PATHS = false>
 __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
+    static_assert(!PATHS || (HA == 1 && !GE && !STAMP && DIAG == 0), "decoded paths: HA 1, E in VGPRs");
     constexpr int HM = kBandHeavy;
     constexpr uint32_t B = 64 * W;
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -143,7 +219,10 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     uint32_t* pcnt = reinterpret_cast<uint32_t*>(pcell + kRing);
     float* junk = reinterpret_cast<float*>(pcnt + kRing);
     float* red = junk + kRing;
-    uint8_t* symr = reinterpret_cast<uint8_t*>(red + 2 * kMaxWaves);
+    uint32_t* jcell = reinterpret_cast<uint32_t*>(red + 2 * kMaxWaves);  // [kRing][2] (8 B aligned)
+    uint32_t* jfin = jcell + 2 * kRing;                                 // [2] (+2 pad)
+    uint32_t* jjunk = jfin + 4;                                         // [16]
+    uint8_t* symr = reinterpret_cast<uint8_t*>(jjunk + 16);
 
     // ---- resident tables ---------------------------------------------------------------------
     // GE == false: et[s][o] = E[o][position t*SM+s] in VGPRs, picked by s_set_gpr_idx.
@@ -194,6 +273,9 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     if (t < kRing) {
         pcell[t] = kInf;
         pcnt[t] = 0;
+    }
+    if constexpr (PATHS) {
+        if (t < 2 * kRing + 4) jcell[t] = 0xFFFFFFFFu;  // jcell and jfin
     }
 
     // ---- sequence ----------------------------------------------------------------------------
@@ -273,10 +355,21 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         if constexpr (PUB1) return wave_min63(pm);  // diagnostic: lane 63 alone publishes
         return row_min16(pm);
     };
-    auto publish = [&](auto slotc, uint32_t obs, float rowmin, float vlast) {
+    // decoded paths: j* cells (wave 0 resets them, other waves hit junk), all-ones reset value
+    uint32_t jcbase = lds_addr(jcell), jrbase = lds_addr(wave ? jjunk : jcell);
+    uint64_t ones64 = ~0ull;
+    if constexpr (PATHS) asm volatile("" : "+v"(jcbase), "+v"(jrbase), "+v"(ones64));
+    auto publish = [&](auto slotc, uint32_t obs, float rowmin, float vlast, uint32_t c0 = ~0u, uint32_t c1 = ~0u) {
         constexpr uint32_t K = decltype(slotc)::value;
-        publish_rows<((K + 2) % kRing) * 4, K * 4, kCntOff + K * 4, K * kMaxWaves * 16>(
-            rbase, cbase, rowmin, bbase, pack(obs + 1u, vlast), inf_v, one, PUB1 ? 0x8000000000000000ull : 0x8000800080008000ull);
+        if constexpr (PATHS) {
+            publish_rows_paths<((K + 2) % kRing) * 4, K * 4, kCntOff + K * 4, K * kMaxWaves * 16,
+                               ((K + 2) % kRing) * 8, K * 8>(
+                rbase, cbase, rowmin, bbase, pack(obs + 1u, vlast), inf_v, one, 0x8000800080008000ull, jrbase,
+                jcbase, c0, c1, ones64);
+        } else {
+            publish_rows<((K + 2) % kRing) * 4, K * 4, kCntOff + K * 4, K * kMaxWaves * 16>(
+                rbase, cbase, rowmin, bbase, pack(obs + 1u, vlast), inf_v, one, PUB1 ? 0x8000000000000000ull : 0x8000800080008000ull);
+        }
     };
     // Arrivals the count of obs's slot has once every row published obs (obs >= first - 1).
     auto arrivals = [&](uint32_t obs) -> uint32_t { return (PUB1 ? 1u : 4u) * W * (((obs + 1u - first) / kRing) + 1u); };
@@ -337,6 +430,76 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         for (int h = 0; h < HM; ++h) vh[h] = vhn[h];
     };
 
+    // ---- decoded paths ------------------------------------------------------------------------
+    // Static lane masks per slot (from pflags): A = only the heavy term exists, B = both exist,
+    // C = both exist and the heavy row has the lower row id (it wins ties).  The light mask of a
+    // slot is then A | (B & [xh < xb]) | (C & [xh == xb]).
+    uint64_t pmA[PATHS ? SM : 1] = {}, pmB[PATHS ? SM : 1] = {}, pmC[PATHS ? SM : 1] = {};
+    uint32_t plr[PATHS ? SM : 1] = {};
+    float vp[PATHS ? SM : 1];  // light scores of the observation before v's (j* search)
+    uint32_t pstage = 0;       // light masks of four observations, staged lane by lane
+    uint32_t* const pmask = PATHS ? reinterpret_cast<uint32_t*>(b.cmask + b.cmask_off[q]) : nullptr;
+    uint32_t* const prec = PATHS ? b.hrec + b.hrec_off[q] : nullptr;
+    if constexpr (PATHS) {
+#pragma unroll
+        for (int s = 0; s < SM; ++s) {
+            const uint32_t f = m.pflags[s * B + t];
+            const bool ec = f & 1u, ea = f & 2u, hl = f & 4u;
+            pmA[s] = __builtin_amdgcn_ballot_w64(ea && !ec);
+            pmB[s] = __builtin_amdgcn_ballot_w64(ea && ec);
+            pmC[s] = __builtin_amdgcn_ballot_w64(ea && ec && hl);
+            plr[s] = m.lrow[s * B + t];
+            vp[s] = kInf;
+        }
+    }
+    // Heavy-row backpointers of observation obs (computed from the previous heavy scores vh and
+    // the light minimum mu, before heavy_update): the lexicographic (value, row) argmin over the
+    // heavy-row terms, and the flag against the light-set term fl(c_A + mu).  Wave 0 stores
+    // record row obs-1.  Returns the light-set targets; `need` = some valid row needs j*.
+    auto heavy_paths = [&](uint32_t obs, float mu, const HeavyConst& hc, float (&tgt)[HM]) -> bool {
+        const float cst[6] = {hc.c0.x, hc.c0.y, hc.c0.z, hc.c0.w, hc.c1.x, hc.c1.y};
+        uint32_t rec2[HM];
+        bool need = false;
+#pragma unroll
+        for (int h = 0; h < HM; ++h) {
+            float hv = kInf;
+            uint32_t hcol = 0x3FFFFFFFu;
+            bool hex = false;
+#pragma unroll
+            for (int k = 0; k < HM; ++k) {
+                if ((m.hx_exist >> (h * HM + k)) & 1u) {
+                    const float val = cst[kBandTailX + h * HM + k] + vh[k];
+                    const uint32_t col = (uint32_t)m.hrow[k];
+                    const bool take = !hex || val < hv || (val == hv && col < hcol);
+                    hv = take ? val : hv;
+                    hcol = take ? col : hcol;
+                    hex = true;
+                }
+            }
+            const bool lex = (m.hl_exist >> h) & 1u;
+            const float lv = cst[kBandTailA + h] + mu;
+            const uint32_t flag = !lex ? (hex ? 0u : 3u) : !hex ? 1u : hv < lv ? 0u : lv < hv ? 1u : 2u;
+            rec2[h] = (flag << 30) | hcol;
+            tgt[h] = lv;
+            need |= m.hvalid[h] && (flag == 1u || flag == 2u);
+        }
+        if (wave == 0 && lane == 0)
+            *reinterpret_cast<uint2*>(prec + (size_t)(obs - 1) * 4) = make_uint2(rec2[0], rec2[1]);
+        return uniform((int)need) != 0;
+    };
+    // j* candidates of this thread: the lowest own light row with fl(c_A + vp[s]) == target.
+    auto jstar_cands = [&](const HeavyConst& hc, const float (&tgt)[HM], uint32_t (&c)[HM]) {
+        const float ca[2] = {hc.c0.x, hc.c0.y};  // cst[kBandTailA + h]
+#pragma unroll
+        for (int h = 0; h < HM; ++h) {
+            uint32_t x = ~0u;
+#pragma unroll
+            for (int s = SM - 1; s >= 0; --s) x = (ca[h] + vp[s] == tgt[h]) ? plr[s] : x;
+            c[h] = x;
+        }
+    };
+    static_assert(kBandTailA == 0 && kBandHeavy == 2, "jstar_cands reads cst[kBandTailA + h] from c0.xy");
+
     float own_p1 = kInf, own_p2 = kInf;  // W == 1: partials of the last two observations
     uint32_t pc_next = 0;                 // W > 1: count and cell of the observation before the
     float pm_next = kInf;                 // current one, read half a step before they are needed
@@ -371,7 +534,34 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
             if (lagged) asm volatile("" : "+v"(pmv), "+v"(pcv));
         }
         mark(1);
-        if (lagged) heavy_update(W > 1 ? take_mu(i - 2, s2, pcv, pmv) : own_p2, hc_prev);  // heavy scores of i-1
+        uint32_t jc[HM] = {~0u, ~0u};  // PATHS: j* candidates of record row i-2
+        uint64_t jword = ~0ull;        // PATHS, wave 0: j* cells of record row i-4
+        bool jvalid = false;
+        if (lagged) {  // heavy scores of i-1
+            const float mu = W > 1 ? take_mu(i - 2, s2, pcv, pmv) : own_p2;
+            if constexpr (PATHS) {
+                float tgt[HM];
+                if (heavy_paths(i - 1, mu, hc_prev, tgt)) jstar_cands(hc_prev, tgt, jc);
+                if constexpr (W > 1) {
+                    // every row's candidates of i-2 arrived with its count (take_mu above)
+                    if (wave == 0 && i >= 4) {
+                        jword = lds_load64(reinterpret_cast<const uint64_t*>(jcell + 2 * s2));
+                        jvalid = true;
+                    }
+                } else {
+#pragma unroll
+                    for (int h = 0; h < HM; ++h) {
+                        const uint32_t r = row_min16_u32(jc[h]);
+                        const uint32_t a = min((uint32_t)__builtin_amdgcn_readlane((int)r, 15),
+                                               (uint32_t)__builtin_amdgcn_readlane((int)r, 31));
+                        const uint32_t c = min((uint32_t)__builtin_amdgcn_readlane((int)r, 47),
+                                               (uint32_t)__builtin_amdgcn_readlane((int)r, 63));
+                        if (lane == 0) prec[(size_t)(i - 2) * 4 + 2 + h] = min(a, c);
+                    }
+                }
+            }
+            heavy_update(mu, hc_prev);
+        }
         if constexpr (W > 1) {  // count first, then the cell of i-1 for the next step (LDS keeps the order)
             pc_next = __hip_atomic_load(pcnt + s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             pm_next = __hip_atomic_load(pcell + s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -388,20 +578,47 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         mark(3);
         pin(vn);  // the light scores first: the boundary word has had the most time to land
         // lane 0, slot 0: the chain predecessor is the left neighbour's last score of i-1
+        float xb0 = xb[0];
         {
             const float bv = take_bnd(i - 1, s1, bwv);
             float r = (e[0] + bw[0]) + bv;
+            if constexpr (PATHS) xb0 = lane == 0 ? r : xb0;
 #pragma unroll
             for (int h = 0; h < HA; ++h) r = fminf(r, xa[h][0] + vh[h]);
             vn[0] = lane == 0 ? r : vn[0];
         }
+        if constexpr (PATHS) {  // light masks of observation i (record row i-1), staged in lanes
+            constexpr uint32_t L0 = ((s0 + kRing - 1) & 3u) * (2 * SM);
+            auto mask_slot = [&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                const float xh = xa[0][s] + vh[0];
+                const float xbe = s == 0 ? xb0 : xb[s];
+                const uint64_t lt = __builtin_amdgcn_ballot_w64(xh < xbe);
+                const uint64_t eq = __builtin_amdgcn_ballot_w64(xh == xbe);
+                const uint64_t code = pmA[s] | (pmB[s] & lt) | (pmC[s] & eq);
+                writelane<L0 + 2 * s>(pstage, (uint32_t)code);
+                writelane<L0 + 2 * s + 1>(pstage, (uint32_t)(code >> 32));
+            };
+            StaticFor<0, SM>::run(mask_slot);
+        }
         if constexpr (W > 1) {
-            publish(slotc, i, row_partial(vn), vn[SM - 1]);
+            if constexpr (PATHS)
+                publish(slotc, i, row_partial(vn), vn[SM - 1], row_min16_u32(jc[0]), row_min16_u32(jc[1]));
+            else
+                publish(slotc, i, row_partial(vn), vn[SM - 1]);
         } else {  // one wave: its own partials are the only ones, keep the last two in registers
             own_p2 = own_p1;
             own_p1 = uniform_f(wave_partial(vn));
         }
         mark(4);
+        if constexpr (PATHS) {
+            if constexpr ((s0 & 3u) == 0) {  // rows i-4 .. i-1 staged: one store per wave
+                if (lane < 8 * SM) pmask[((size_t)((i - 1) >> 2) * W + wave) * (8 * SM) + lane] = pstage;
+            }
+            if (jvalid && lane == 0) *reinterpret_cast<uint64_t*>(prec + (size_t)(i - 4) * 4 + 2) = jword;
+#pragma unroll
+            for (int s = 0; s < SM; ++s) vp[s] = v[s];
+        }
 #pragma unroll
         for (int s = 0; s < SM; ++s) v[s] = vn[s];
         return hc;
@@ -497,7 +714,38 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         const uint32_t sl = (len - 2) & (kRing - 1);
         float mu = own_p2;
         if constexpr (W > 1) mu = take_mu(len - 2, sl, pc_next, pm_next);
+        if constexpr (PATHS) {  // record row len-2: its j* straight from the kept scores v_{len-2}
+            float tgt[HM];
+            uint32_t jc[HM] = {~0u, ~0u};
+            if (heavy_paths(len - 1, mu, hc, tgt)) jstar_cands(hc, tgt, jc);
+#pragma unroll
+            for (int h = 0; h < HM; ++h) {
+                const uint32_t r = row_min16_u32(jc[h]);
+                if ((lane & 15u) == 15u)
+                    __hip_atomic_fetch_min(jfin + h, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
         heavy_update(mu, hc);
+    }
+    if constexpr (PATHS) {
+        if (len > 1 && ((len - 1) & 3u) != 0 && lane < 8 * SM)  // the last, partial block of masks
+            pmask[((size_t)((len - 2) >> 2) * W + wave) * (8 * SM) + lane] = pstage;
+        __syncthreads();  // every wave's j* candidates are in
+        if (wave == 0 && lane == 0 && len > 1) {  // rows the loop did not store (W > 1: len-4, len-3)
+            uint32_t* rr = prec + (size_t)(len - 2) * 4 + 2;
+            rr[0] = jfin[0];
+            rr[1] = jfin[1];
+            if (W > 1 && len >= 3) {
+                const uint32_t* c = jcell + 2 * ((len - 1) & (kRing - 1));
+                prec[(size_t)(len - 3) * 4 + 2] = c[0];
+                prec[(size_t)(len - 3) * 4 + 3] = c[1];
+            }
+            if (W > 1 && len >= 4) {
+                const uint32_t* c = jcell + 2 * ((len - 2) & (kRing - 1));
+                prec[(size_t)(len - 4) * 4 + 2] = c[0];
+                prec[(size_t)(len - 4) * 4 + 3] = c[1];
+            }
+        }
     }
 
     if (lane == 0 && m.stamps) {  // diagnostics (SVH_BAND_DEBUG & 4: segment stamps, & 128: spins only)
@@ -563,50 +811,13 @@ const void* chain_ptr_w(int sm, bool ge) {
         default: return nullptr;
     }
 }
-template <int HA>
-const void* chain_ptr(int sm, int waves, bool ge) {
-    switch (waves) {
-        case 1: return chain_ptr_w<1, HA>(sm, ge);
-        case 2: return chain_ptr_w<2, HA>(sm, ge);
-        case 4: return chain_ptr_w<4, HA>(sm, ge);
-        case 8: return chain_ptr_w<8, HA>(sm, ge);
-        default: return nullptr;
-    }
-}
-const void* chain_fn(int sm, int waves, int ha, bool ge) {
-    return ha == 1 ? chain_ptr<1>(sm, waves, ge) : ha == 2 ? chain_ptr<2>(sm, waves, ge) : nullptr;
-}
 
 }  // namespace
 
-bool chain_supported(int sm, int waves, int ha, bool ge) { return chain_fn(sm, waves, ha, ge) != nullptr; }
-
-hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStream_t stream) {
-    const int waves = (int)(m.B / 64);
-    const bool ge = m.ge != 0;
-    const void* fn = chain_fn((int)m.SM, waves, ha, ge);
-    if ((m.dbg & 4u) && ha == 1) {  // diagnostic stamp builds
-        if (!ge && m.SM == 5 && waves == 8) fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, true>);
-        if (!ge && m.SM == 5 && waves == 1) fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 1, 1, false, true>);
-        if (ge && m.SM == 10 && waves == 4) fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<10, 4, 1, true, true>);
-    }
-    if ((m.dbg & (64u | 2048u | 4096u)) && ha == 1 && !ge && m.SM == 5 && waves == 8) {  // diagnostic ablations
-        switch (((m.dbg >> 6) & 1u) | ((m.dbg >> 10) & 6u)) {
-            case 1: fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, false, 1>); break;
-            case 2: fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, false, 2>); break;
-            case 4: fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, false, 4>); break;
-            case 6: fn = reinterpret_cast<const void*>(&chain_viterbi_kernel<5, 8, 1, false, false, 6>); break;
-            default: break;
-        }
-    }
-    if (!fn || m.B % 64 || m.S > (uint32_t)kChainMaxSym || m.erow < m.SM * m.B + kBandTail ||
-        (ge && !m.erows_t))
-        return hipErrorInvalidValue;
-    if (b.nseq == 0) return hipSuccess;
-    BandModel mm = m;
-    FusedBatch bb = b;
-    void* args[] = {&mm, &bb};
-    return hipLaunchKernel(fn, dim3(b.nseq), dim3(m.B), args, chain_lds_bytes(), stream);
-}
+// Instantiation tables, one translation unit each (they compile in parallel).
+const void* chain_fn_ha1(int sm, int waves, bool ge);    // chain_ha1.hip
+const void* chain_fn_ha2(int sm, int waves, bool ge);    // chain_ha2.hip
+const void* chain_diag_fn(int sm, int waves, bool ge, uint32_t dbg);  // chain_ha1.hip: stamps, ablations
+const void* chain_paths_fn(int sm, int waves);           // chain_paths.hip
 
 }  // namespace svh

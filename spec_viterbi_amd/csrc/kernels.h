@@ -56,6 +56,16 @@ struct FusedBatch {
     int64_t* best;             // [nseq] lowest-index argmin of final scores (nullable)
     uint16_t* bp;              // backpointers (PATHS only)
     const uint64_t* bp_off;    // [nseq] element offset of sequence q's (len-1) x n block
+    // Chain-kernel decoded paths (chain.hip): per backpointer row r (observation r+1)
+    //   cmask: one 64-bit lane mask per (wave, slot): bit = "light position took its heavy term";
+    //          layout [r/4][wave][r%4][slot] u64, blocks of four rows
+    //   hrec:  [r][4] u32: [h] = flag<<30 | row of the heavy-term argmin of heavy row h,
+    //          [2+h] = j*, the lowest light row achieving the light-set minimum of heavy row h
+    //          (flag 0: heavy term wins, 1: light set wins, 2: tie, 3: no term; see chain.hip)
+    uint64_t* cmask;
+    const uint64_t* cmask_off;  // [nseq] u64 offset of sequence q's masks
+    uint32_t* hrec;
+    const uint64_t* hrec_off;   // [nseq] u32 offset of sequence q's records
     uint32_t nseq;
 };
 
@@ -95,6 +105,12 @@ struct BandModel {
                    // 16 chain kernel ignores the exchange tags (never waits)
     unsigned long long* stamps;  // [nseq][kMaxWaves][kBandStamps] cycle sums (dbg & 4)
     uint32_t* fault;             // chain kernel: set non-zero if a bounded spin gave up
+    // decoded paths (chain kernel, HA <= 1):
+    const uint8_t* pflags;  // [SM*B] bit0: term from position p-1 exists, bit1: term from heavy
+                            // row 0 exists, bit2: heavy row 0 < row of p-1 (heavy wins ties)
+    const int32_t* spos;    // [n] position of a light row, -1-h for heavy row h
+    uint32_t hx_exist;      // bit h*kBandHeavy+k: heavy row k -> heavy row h term exists
+    uint32_t hl_exist;      // bit h: heavy row h has the shared term from every light row
 };
 constexpr int kBandStamps = 8;
 
@@ -106,13 +122,25 @@ constexpr uint32_t kChainSymChunk = 32768;  // symbols staged in LDS per refill
 constexpr int kChainRing = 8;  // exchange ring depth (observations in flight between waves)
 inline size_t chain_lds_bytes() {
     // heavy constants | tagged records [ring][waves][2] u64 | cells, counts, junk [ring] 4 B each |
-    // reduction | staged symbols
+    // reduction | path cells: j* [ring][2], final [2] + pad, junk [16] (u32) | staged symbols
     return (size_t)kChainMaxSym * kBandTail * sizeof(float) + (size_t)kChainRing * 2 * kMaxWaves * 8 +
-           3 * kChainRing * 4 + 2 * kMaxWaves * sizeof(float) + kChainSymChunk;
+           3 * kChainRing * 4 + 2 * kMaxWaves * sizeof(float) + (2 * kChainRing + 4 + 16) * 4 +
+           kChainSymChunk;
 }
 // Chain kernel for (SM slots, W waves, HA heavy feeders, E streamed?); false if not instantiated.
 bool chain_supported(int sm, int waves, int ha, bool ge);
+// Decoded-path variant (E in VGPRs, HA <= 1) instantiated for this geometry?
+bool chain_paths_supported(int sm, int waves);
+// b.cmask != nullptr selects the decoded-path variant (every sequence must start at step 0).
 hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStream_t stream);
+// Path traceback over the chain kernel's compact backpointers (one wave per sequence).
+hipError_t launch_chain_traceback(const BandModel& m, const FusedBatch& b, const uint64_t* path_off,
+                                  int32_t* paths, hipStream_t stream);
+// u64 masks / u32 records the decoded-path variant writes for a sequence of length len.
+inline uint64_t chain_mask_words(uint64_t len, uint32_t waves, uint32_t sm) {
+    return len > 1 ? (len - 1 + 3) / 4 * 4 * (uint64_t)waves * sm : 0;
+}
+inline uint64_t chain_hrec_words(uint64_t len) { return len > 1 ? (len - 1) * 4 : 0; }
 
 // CSR of T^T used by the generic kernel and the _spec precompute.
 struct CsrModel {

@@ -358,15 +358,19 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
     std::vector<float> bwp(nL, kInfH);
     std::vector<std::vector<float>> awp(heavy.size(), std::vector<float>(nL, kInfH));
     std::vector<uint8_t> feeds(heavy.size(), 0);
+    std::vector<uint8_t> bex(nL, 0);                                            // term p-1 -> p exists
+    std::vector<std::vector<uint8_t>> aex(heavy.size(), std::vector<uint8_t>(nL, 0));  // heavy -> p
     for (uint32_t p = 0; p < nL; ++p) {
         const uint32_t j = light[p];
         for (uint32_t e = hm.rowptr[j]; e < hm.rowptr[j + 1]; ++e) {
             const uint32_t k = hm.col[e];
             if (hidx[k] >= 0) {
                 awp[hidx[k]][p] = hm.val[e];
+                aex[hidx[k]][p] = 1;
                 feeds[hidx[k]] = 1;
             } else if (p > 0 && pos[k] == p - 1) {
                 bwp[p] = hm.val[e];
+                bex[p] = 1;
             } else {
                 return bp;
             }
@@ -403,6 +407,8 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
         if (exc[x].size() > (size_t)kBandHeavy) return bp;  // cannot happen: one term per source
         if (nlight != 0 && (nlight != nL || !same)) return bp;
         wh[x] = nlight ? w : kInfH;
+        if (nlight) bp.hl_exist |= 1u << x;
+        for (const auto& e : exc[x]) bp.hx_exist |= 1u << (x * kBandHeavy + e.first);
     }
 
     uint32_t SM = 0, B = 0;
@@ -470,13 +476,23 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
     bp.start.assign(cap, kInfH);
     bp.bw.assign(cap, kInfH);
     bp.aw.assign((size_t)std::max<uint32_t>(HA, 1) * cap, kInfH);
+    // decoded paths: per-position term flags (heavy feeder 0 only: the path variant has HA <= 1)
+    // and the state -> position / heavy index map of the traceback
+    bp.pflags.assign(cap, 0);
+    bp.spos.assign(n, 0);
     for (uint32_t p = 0; p < nL; ++p) {
         const uint32_t x = slot_of(p);
         bp.lrow[x] = light[p];
         bp.start[x] = hm.start[light[p]];
         bp.bw[x] = bwp[p];
         for (uint32_t a = 0; a < HA; ++a) bp.aw[(size_t)a * cap + x] = awp[order[a]][p];
+        uint8_t f = bex[p] ? 1 : 0;
+        if (HA >= 1 && aex[order[0]][p]) f |= 2;
+        if (HA >= 1 && p > 0 && heavy[order[0]] < light[p - 1]) f |= 4;
+        bp.pflags[x] = f;
+        bp.spos[light[p]] = (int32_t)p;
     }
+    for (size_t x = 0; x < order.size(); ++x) bp.spos[heavy[order[x]]] = -1 - (int32_t)x;
     // streamed-E chain kernel: [o][t][round_up(SM,4)]
     if (ge) {
         const uint32_t smp = (SM + 3) / 4 * 4;
@@ -512,6 +528,8 @@ void DeviceBandPlan::upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream
     d_bw.upload(p.bw.data(), p.bw.size() * 4, s);
     d_lrow.upload(p.lrow.data(), p.lrow.size() * 4, s);
     if (p.ge) d_erows_t.upload(p.erows_t.data(), p.erows_t.size() * 4, s);
+    d_pflags.upload(p.pflags.data(), p.pflags.size(), s);
+    d_spos.upload(p.spos.data(), p.spos.size() * 4, s);
     std::memset(&view, 0, sizeof(view));
     view.erows = d_erows.as<float>();
     view.start = d_start.as<float>();
@@ -520,6 +538,10 @@ void DeviceBandPlan::upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream
     view.lrow = d_lrow.as<uint32_t>();
     view.erows_t = p.ge ? d_erows_t.as<float>() : nullptr;
     view.ge = p.ge ? 1u : 0u;
+    view.pflags = d_pflags.as<uint8_t>();
+    view.spos = d_spos.as<int32_t>();
+    view.hx_exist = p.hx_exist;
+    view.hl_exist = p.hl_exist;
     for (int h = 0; h < kBandHeavy; ++h) {
         view.hrow[h] = p.hrow[h];
         view.hvalid[h] = p.hvalid[h];
@@ -671,9 +693,11 @@ CsrModel Model::csr_view() const {
 }
 
 const DeviceBandPlan* Model::band_for(bool paths) const {
-    if (paths || !band.plan.ok) return nullptr;
-    return (kernel_pref == SVH_KERNEL_AUTO || kernel_pref == SVH_KERNEL_BAND ||
-            kernel_pref == SVH_KERNEL_CHAIN) ? &band : nullptr;
+    if (!band.plan.ok) return nullptr;
+    if (kernel_pref != SVH_KERNEL_AUTO && kernel_pref != SVH_KERNEL_BAND && kernel_pref != SVH_KERNEL_CHAIN)
+        return nullptr;
+    if (paths) return band.plan.paths_ok() ? &band : nullptr;  // decoded-path chain variant
+    return &band;
 }
 
 const DevicePlan* Model::plan_for(bool paths) const {
@@ -756,6 +780,7 @@ svh_model_info Model::info() const {
     }
     i.spec_level = spec_level;
     i.spec_bytes = d_products.bytes;
+    i.paths_kernel = band_for(true) ? SVH_KERNEL_CHAIN : plan_for(true) ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
     return i;
 }
 
@@ -770,11 +795,14 @@ Batch::Batch(Model* m, uint64_t nseq_, const uint64_t* offs, const uint64_t* sym
     if (!offs || !symbols) throw Error(SVH_E_INVALID, "null offsets/symbols");
     nseq = (uint32_t)nseq_;
     paths = (flags & SVH_BATCH_PATHS) != 0;
-    if (paths && m->host.n >= kNoPred) throw Error(SVH_E_UNSUPPORTED, "paths need states_num < 65535");
+    const DeviceBandPlan* cpl = paths ? m->band_for(true) : nullptr;
+    chain_paths = cpl != nullptr;
+    if (paths && !chain_paths && m->host.n >= kNoPred)
+        throw Error(SVH_E_UNSUPPORTED, "paths need states_num < 65535 for models the chain kernel does not cover");
     offsets.assign(offs, offs + nseq + 1);
     lens.resize(nseq);
-    std::vector<uint64_t> symoff(nseq), bpoff(nseq), pathoff(nseq);
-    uint64_t bytes = 0, bpn = 0;
+    std::vector<uint64_t> symoff(nseq), bpoff(nseq), pathoff(nseq), cmoff(nseq), hroff(nseq);
+    uint64_t bytes = 0, bpn = 0, cmn = 0, hrn = 0;
     for (uint32_t q = 0; q < nseq; ++q) {
         if (offs[q + 1] < offs[q]) throw Error(SVH_E_INVALID, "offsets must be non-decreasing");
         const uint64_t len = offs[q + 1] - offs[q];
@@ -784,8 +812,15 @@ Batch::Batch(Model* m, uint64_t nseq_, const uint64_t* offs, const uint64_t* sym
         lens[q] = (uint32_t)len;
         symoff[q] = bytes;
         bytes += ((len + kSymPad + 4 + 15) / 16) * 16;
-        bpoff[q] = bpn;
-        bpn += (len - 1) * (uint64_t)m->host.n;
+        if (chain_paths) {
+            cmoff[q] = cmn;
+            cmn += chain_mask_words(len, cpl->plan.B / 64, cpl->plan.SM);
+            hroff[q] = hrn;
+            hrn += chain_hrec_words(len);
+        } else {
+            bpoff[q] = bpn;
+            bpn += (len - 1) * (uint64_t)m->host.n;
+        }
         pathoff[q] = offs[q] - offs[0];
     }
     total = offs[nseq] - offs[0];
@@ -810,9 +845,16 @@ Batch::Batch(Model* m, uint64_t nseq_, const uint64_t* offs, const uint64_t* sym
     d_end.upload(lens.data(), lens.size() * 4, s);
     d_scores.alloc((size_t)nseq * m->host.n * 4);
     d_best.alloc((size_t)nseq * 8);
-    if (paths) {
-        d_bp.alloc((size_t)bpn * 2);
+    if (paths && chain_paths) {
+        d_cmask.alloc((size_t)std::max<uint64_t>(cmn, 1) * 8);
+        d_cmaskoff.upload(cmoff.data(), cmoff.size() * 8, s);
+        d_hrec.alloc((size_t)std::max<uint64_t>(hrn, 4) * 4);
+        d_hrecoff.upload(hroff.data(), hroff.size() * 8, s);
+    } else if (paths) {
+        d_bp.alloc((size_t)std::max<uint64_t>(bpn, 1) * 2);
         d_bpoff.upload(bpoff.data(), bpoff.size() * 8, s);
+    }
+    if (paths) {
         d_pathoff.upload(pathoff.data(), pathoff.size() * 8, s);
         d_paths.alloc((size_t)total * 4);
     }
@@ -846,7 +888,12 @@ void Batch::run(uint32_t level, hipStream_t s) {
     fb.scores = d_scores.as<float>();
     fb.best = d_best.as<int64_t>();
     fb.nseq = nseq;
-    if (paths) {
+    if (paths && chain_paths) {
+        fb.cmask = d_cmask.as<uint64_t>();
+        fb.cmask_off = d_cmaskoff.as<uint64_t>();
+        fb.hrec = d_hrec.as<uint32_t>();
+        fb.hrec_off = d_hrecoff.as<uint64_t>();
+    } else if (paths) {
         fb.bp = d_bp.as<uint16_t>();
         fb.bp_off = d_bpoff.as<uint64_t>();
     }
@@ -872,9 +919,13 @@ void Batch::run(uint32_t level, hipStream_t s) {
     hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
     if (level <= 1) {
         launch_step_kernel(fb, paths);
-        if (paths) hip_check(launch_traceback(fb, d_pathoff.as<uint64_t>(), d_paths.as<int32_t>(),
-                                              model->host.n, s),
-                             "traceback kernel");
+        if (paths && chain_paths)
+            hip_check(launch_chain_traceback(model->band_for(true)->view, fb, d_pathoff.as<uint64_t>(),
+                                             d_paths.as<int32_t>(), s),
+                      "chain traceback kernel");
+        else if (paths)
+            hip_check(launch_traceback(fb, d_pathoff.as<uint64_t>(), d_paths.as<int32_t>(), model->host.n, s),
+                      "traceback kernel");
     } else {
         const uint32_t n = model->host.n;
         if (spec_ready_level != level) {

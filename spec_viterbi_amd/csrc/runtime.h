@@ -105,13 +105,18 @@ struct BandPlan {
     float hstart[kBandHeavy] = {0, 0};
     std::vector<float> erows, erows_t, start, aw, bw;
     std::vector<uint32_t> lrow;
+    std::vector<uint8_t> pflags;  // decoded paths (BandModel::pflags)
+    std::vector<int32_t> spos;    // decoded paths (BandModel::spos)
+    uint32_t hx_exist = 0, hl_exist = 0;
     size_t lds_bytes = 0;
+    // the decoded-path chain variant can run this plan
+    bool paths_ok() const { return ok && chain && !ge && HA <= 1 && chain_paths_supported((int)SM, (int)(B / 64)); }
 };
 BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain);
 
 struct DeviceBandPlan {
     BandPlan plan;
-    DeviceBuffer d_erows, d_erows_t, d_start, d_aw, d_bw, d_lrow, d_stamps, d_fault;
+    DeviceBuffer d_erows, d_erows_t, d_start, d_aw, d_bw, d_lrow, d_stamps, d_fault, d_pflags, d_spos;
     BandModel view{};
     void upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream_t s);
     void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_BAND_DEBUG & 4)
@@ -153,6 +158,8 @@ struct Batch {
     uint64_t total = 0;
     DeviceBuffer d_sym, d_symoff, d_begin, d_end, d_scores, d_best;
     DeviceBuffer d_bp, d_bpoff, d_pathoff, d_paths;
+    bool chain_paths = false;  // paths from the chain kernel's compact records (else fused / generic)
+    DeviceBuffer d_cmask, d_cmaskoff, d_hrec, d_hrecoff;
     // _spec runs
     DeviceBuffer d_vbuf, d_nchunks, d_tbegin, d_vrow;
     uint32_t spec_ready_level = 0;

@@ -93,11 +93,13 @@ def random_seqs(S, lengths, seed=0):
 
 
 def random_chain_hmm(L, S=20, seed=0, self_n=True, self_c=True, feed_c=False, c_from_m=True, n_from_m=True,
-                     zero_emis=0.0, gap=None, start=(0,), **_):
+                     zero_emis=0.0, gap=None, start=(0,), ties=False, inf_edges=0.0, **_):
     """MSV-shaped random model (the shape chmm_files/silent_hmm_to_chmm.py writes): N=0, M_1..M_L,
     C=L+1.  N -> M_j, M_j -> M_{j+1}, M_j -> N and M_j -> C with one shared weight each, N and C
     self loops.  Variants: feed_c adds C -> M_j (light rows fed by two heavy rows); c_from_m /
-    n_from_m drop the uniform M -> heavy terms; gap drops M_gap -> M_gap+1 (chain break)."""
+    n_from_m drop the uniform M -> heavy terms; gap drops M_gap -> M_gap+1 (chain break); ties draws
+    every probability from {1/2, 1/4, 1/8} (integer scores: exact ties everywhere); inf_edges sets
+    that fraction of the light rows' terms to probability 0 (the term exists, weight +inf)."""
     from spec_viterbi_amd import HMM
 
     rng = np.random.default_rng(seed)
@@ -105,12 +107,18 @@ def random_chain_hmm(L, S=20, seed=0, self_n=True, self_c=True, feed_c=False, c_
     C = L + 1
     src, dst, pr = [], [], []
 
-    def add(a, b, p):
+    def add(a, b, p, shared=False):
+        if ties and not shared:
+            p = float(rng.choice([0.5, 0.25, 0.125]))
+        if inf_edges > 0 and b not in (0, C) and rng.random() < inf_edges:
+            p = 0.0
         src.append(a)
         dst.append(b)
         pr.append(np.float32(p))
 
     w_n, w_c = rng.uniform(0.01, 0.2), rng.uniform(0.01, 0.2)
+    if ties:
+        w_n, w_c = float(rng.choice([0.5, 0.25, 0.125])), float(rng.choice([0.5, 0.25, 0.125]))
     for j in range(1, L + 1):
         add(0, j, rng.uniform(0.001, 0.05))
         if feed_c:
@@ -118,14 +126,16 @@ def random_chain_hmm(L, S=20, seed=0, self_n=True, self_c=True, feed_c=False, c_
         if j < L and j != gap:
             add(j, j + 1, rng.uniform(0.3, 0.9))
         if n_from_m:
-            add(j, 0, w_n)
+            add(j, 0, w_n, shared=True)
         if c_from_m:
-            add(j, C, w_c)
+            add(j, C, w_c, shared=True)
     if self_n:
         add(0, 0, rng.uniform(0.5, 0.99))
     if self_c:
         add(C, C, rng.uniform(0.5, 0.99))
     em = rng.uniform(0.001, 1.0, size=(S, n)).astype(np.float32)
+    if ties:
+        em = rng.choice(np.array([0.5, 0.25, 0.125], np.float32), size=(S, n))
     if zero_emis > 0:
         em[rng.random(em.shape) < zero_emis] = 0.0
 

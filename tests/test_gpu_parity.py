@@ -225,7 +225,66 @@ def test_chain_random_models(L, kw, seed):
     check_against_oracle(hmm, seqs, paths=False)
     if L >= 2:
         check_against_oracle(hmm, seqs, kernel=_lib.SVH_KERNEL_BAND, paths=False)
-    check_against_oracle(hmm, seqs[:4], paths=True)  # paths go through the fused kernel
+    check_against_oracle(hmm, seqs[:4], paths=True)
+
+
+@pytest.mark.parametrize("L,kw,seed", [
+    (1, {}, 1), (2, {}, 2), (63, {}, 3), (64, {}, 4), (65, {}, 5), (700, {}, 6), (2560, {}, 7),
+    (300, {"self_n": False, "self_c": False}, 9),     # no heavy-heavy terms
+    (300, {"c_from_m": False}, 10),                   # a heavy row without light sources
+    (300, {"zero_emis": 0.2}, 11),                    # +inf emissions
+    (300, {"start": (0, 5, 301)}, 12),                # start in light and heavy rows
+    (300, {"gap": 150}, 13),                          # chain break (no predecessor term)
+    (300, {"ties": True}, 17),                        # integer scores: ties everywhere
+    (1000, {"ties": True, "zero_emis": 0.1}, 18),
+    (300, {"inf_edges": 0.3}, 19),                    # terms of weight +inf
+    (300, {"inf_edges": 0.3, "ties": True, "start": (0, 7)}, 20),
+    (300, {"feed_c": True}, 8),                       # two heavy feeders: fused paths
+])
+def test_chain_decoded_paths(L, kw, seed):
+    """Decoded paths from the chain kernel's compact records (light lane masks, heavy-row records
+    with the j* second pass) and the speculative traceback: scores, best states and every path
+    entry identical to the oracle's lexicographic (value, row) argmin, over lengths 1..5000."""
+    hmm = random_chain_hmm(L, seed=seed, **kw)
+    seqs = random_seqs(20, [1, 2, 3, 4, 5, 6, 7, 8, 9, 63, 64, 65, 77, 1000, 5000], seed=seed)
+    model = check_against_oracle(hmm, seqs, paths=True)
+    want = _lib.SVH_KERNEL_FUSED if kw.get("feed_c") else _lib.SVH_KERNEL_CHAIN
+    if L >= 2:
+        assert model.info()["paths_kernel"] == want, model.info()
+
+
+def test_chain_paths_covid_2405():
+    """covid-19.ess (38..7096 observations, symbol refills) on 2405.chmm: chain decoded paths."""
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("covid-19.ess"))
+    model = check_against_oracle(hmm, seqs, paths=True)
+    assert model.info()["paths_kernel"] == _lib.SVH_KERNEL_CHAIN
+
+
+@pytest.mark.parametrize("threads", [64, 128, 256, 512])
+def test_chain_paths_geometries(threads):
+    hmm = svh.read_HMM(chmm("300.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    model = check_against_oracle(hmm, seqs, max_threads=threads, paths=True)
+    assert model.info()["paths_kernel"] == _lib.SVH_KERNEL_CHAIN
+
+
+def test_chain_paths_match_fused_paths():
+    """The two decoded-path implementations agree on every reference .chmm (emit_3_3500_20)."""
+    seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    for name in sorted(os.listdir(os.path.dirname(chmm("2405.chmm")))):
+        if not name.endswith(".chmm"):
+            continue
+        hmm = svh.read_HMM(chmm(name))
+        a = svh.DeviceModel(hmm)
+        if a.info()["paths_kernel"] != _lib.SVH_KERNEL_CHAIN:
+            continue
+        b = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_FUSED)
+        sa, ba, pa = a.viterbi(seqs, paths=True)
+        sb, bb, pb = b.viterbi(seqs, paths=True)
+        assert bit_equal(sa, sb) and np.array_equal(ba, bb), name
+        for q in range(len(seqs)):
+            assert np.array_equal(pa[q], pb[q]), (name, q)
 
 
 def test_chain_covid_many_sequences_and_resume():
