@@ -115,10 +115,19 @@ __device__ __forceinline__ float row_min16(float x) {
     return x;
 }
 
-// dst[L] = x (x wave-uniform, in an SGPR; the lane an inline constant: one constant-bus read)
+// dst[L] = x (x wave-uniform, in an SGPR; the lane an inline constant: one constant-bus read).
+// x must be written by an SALU instruction (mask_code below): read straight after the VALU
+// compare that wrote it, v_writelane took a stale value on MI355X (wrong lane masks), and hipcc
+// pads no hazard for an asm consumer.
 template <uint32_t L>
 __device__ __forceinline__ void writelane(uint32_t& dst, uint32_t x) {
     asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(x), "n"(L));
+}
+// lt | (c & eq) on SALU (see writelane)
+__device__ __forceinline__ uint64_t mask_code(uint64_t lt, uint64_t eq, uint64_t c) {
+    uint64_t r;
+    asm volatile("s_and_b64 %0, %2, %3\n\ts_or_b64 %0, %0, %1" : "=&s"(r) : "s"(lt), "s"(eq), "s"(c) : "scc");
+    return r;
 }
 
 // f(integral_constant<int, I>) for I in [I0, N): a loop whose index is a constant expression
@@ -187,15 +196,17 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 
 // PATHS (decoded paths; HA <= 1, every sequence starts at step 0) adds the backpointers of every
-// observation, in the order of the oracle's lexicographic (value, row) argmin:
+// observation, in the order of the oracle's lexicographic (value, row) argmin.  All of it runs
+// after the observation's publish, off the inter-wave critical path:
 //   * light position p: its two candidates (position p-1, heavy row 0) are compared in every lane
 //     and one 64-bit lane mask per slot records "took the heavy term" (staged in a VGPR by
 //     v_writelane, stored every four observations);
-//   * heavy row h: the heavy-term argmin and the flag heavy / light / tie / none are decided where
-//     the heavy scores are (every thread, redundantly; wave 0 stores them).  The light-set argmin
-//     j* = the lowest light row with fl(c + v[j]) == fl(c + min v) is a second pass over the
-//     light scores once the minimum is known: two observations later, over a kept copy of the
-//     scores, reduced through two more LDS min cells published before the arrival count.
+//   * heavy row h: the heavy-term argmin and the flag heavy / light / tie / none are decided from
+//     the heavy scores every thread holds (wave 0 stores them).  The light-set argmin j* = the
+//     lowest light position with fl(c + v[j]) == fl(c + min v) is a second pass over a kept copy
+//     of the light scores, run only when some flag needs it (rare: on 2405.chmm about 20 of
+//     3500 observations), reduced through two LDS min cells published with the next
+//     observation's exchange, before its arrival count.
 template <int SM, int W, int HA, bool GE, bool STAMP = false, int DIAG = 0, bool PATHS = false>
 __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
     static_assert(!PATHS || (HA == 1 && !GE && !STAMP && DIAG == 0), "decoded paths: HA 1, E in VGPRs");
@@ -223,6 +234,9 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     uint32_t* jfin = jcell + 2 * kRing;                                 // [2] (+2 pad)
     uint32_t* jjunk = jfin + 4;                                         // [16]
     uint8_t* symr = reinterpret_cast<uint8_t*>(jjunk + 16);
+    // PATHS: the light scores of the last two observations, [i & 1][s * B + t] (each lane reads
+    // back only its own: a per-lane spill, no inter-wave order needed)
+    float* vkeep = reinterpret_cast<float*>(symr + kChainSymChunk);
 
     // ---- resident tables ---------------------------------------------------------------------
     // GE == false: et[s][o] = E[o][position t*SM+s] in VGPRs, picked by s_set_gpr_idx.
@@ -431,75 +445,87 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     };
 
     // ---- decoded paths ------------------------------------------------------------------------
-    // Static lane masks per slot (from pflags): A = only the heavy term exists, B = both exist,
-    // C = both exist and the heavy row has the lower row id (it wins ties).  The light mask of a
-    // slot is then A | (B & [xh < xb]) | (C & [xh == xb]).
-    uint64_t pmA[PATHS ? SM : 1] = {}, pmB[PATHS ? SM : 1] = {}, pmC[PATHS ? SM : 1] = {};
-    uint32_t plr[PATHS ? SM : 1] = {};
-    float vp[PATHS ? SM : 1];  // light scores of the observation before v's (j* search)
+    // Static lane mask per slot (from pflags): C = the heavy term exists and wins ties (it has the
+    // lower row id, or there is no chain term).  The light mask of a slot is [xh < xb] | (C &
+    // [xh == xb]): without a heavy term xh = +inf is never below xb and C drops the tie; without
+    // a chain term xb = +inf, so the heavy term is taken.
+    //
+    // Output staging: nothing is stored to HBM inside the loop except one flush per 32
+    // observations.  The masks go to an LDS ring per wave (mring [wave][64 rows][SM] u64, four
+    // rows per ds_write), the heavy records to an LDS ring written by wave 0 (hring [64 rows][4]).
+    // A global store inside the loop would make any later vmcnt(0) wait (a spill reload's, say)
+    // wait for that store to reach memory.
+    uint64_t pmC[PATHS ? SM : 1] = {};
+    uint32_t* const mring = reinterpret_cast<uint32_t*>(vkeep + 2 * SM * B);  // u64 pairs
+    uint32_t* const hring = mring + 2 * W * kPathRing * SM;
+    const uint32_t pos0 = t * SM;  // position of slot 0
     uint32_t pstage = 0;       // light masks of four observations, staged lane by lane
-    uint32_t* const pmask = PATHS ? reinterpret_cast<uint32_t*>(b.cmask + b.cmask_off[q]) : nullptr;
-    uint32_t* const prec = PATHS ? b.hrec + b.hrec_off[q] : nullptr;
     if constexpr (PATHS) {
 #pragma unroll
         for (int s = 0; s < SM; ++s) {
             const uint32_t f = m.pflags[s * B + t];
             const bool ec = f & 1u, ea = f & 2u, hl = f & 4u;
-            pmA[s] = __builtin_amdgcn_ballot_w64(ea && !ec);
-            pmB[s] = __builtin_amdgcn_ballot_w64(ea && ec);
-            pmC[s] = __builtin_amdgcn_ballot_w64(ea && ec && hl);
-            plr[s] = m.lrow[s * B + t];
-            vp[s] = kInf;
+            pmC[s] = __builtin_amdgcn_ballot_w64(ea && (!ec || hl));
+            vkeep[s * B + t] = v[s];  // v_0 (the loop keeps v_i at [i & 1])
         }
     }
-    // Heavy-row backpointers of observation obs (computed from the previous heavy scores vh and
-    // the light minimum mu, before heavy_update): the lexicographic (value, row) argmin over the
-    // heavy-row terms, and the flag against the light-set term fl(c_A + mu).  Wave 0 stores
-    // record row obs-1.  Returns the light-set targets; `need` = some valid row needs j*.
-    auto heavy_paths = [&](uint32_t obs, float mu, const HeavyConst& hc, float (&tgt)[HM]) -> bool {
-        const float cst[6] = {hc.c0.x, hc.c0.y, hc.c0.z, hc.c0.w, hc.c1.x, hc.c1.y};
-        uint32_t rec2[HM];
+    // Heavy-row record of observation obs (record row obs-1): the inputs of its backpointers --
+    // the heavy scores vo of obs-1 and the light minimum mu of obs-1 -- stored by wave 0; the
+    // traceback re-evaluates the lexicographic (value, row) argmin from them with the same float
+    // operations, only where a path passes.  Here only `need` is decided: a valid heavy row whose
+    // new score came from its light-set term (won or tied), so j* must be found.  tgt[h] is that
+    // term, fl(c_A + mu).
+    auto heavy_record = [&](uint32_t obs, float mu, const HeavyConst& hc, const float (&vo)[HM],
+                            float (&tgt)[HM]) -> bool {
+        const float ca[2] = {hc.c0.x, hc.c0.y};  // cst[kBandTailA + h]
         bool need = false;
 #pragma unroll
         for (int h = 0; h < HM; ++h) {
-            float hv = kInf;
-            uint32_t hcol = 0x3FFFFFFFu;
-            bool hex = false;
-#pragma unroll
-            for (int k = 0; k < HM; ++k) {
-                if ((m.hx_exist >> (h * HM + k)) & 1u) {
-                    const float val = cst[kBandTailX + h * HM + k] + vh[k];
-                    const uint32_t col = (uint32_t)m.hrow[k];
-                    const bool take = !hex || val < hv || (val == hv && col < hcol);
-                    hv = take ? val : hv;
-                    hcol = take ? col : hcol;
-                    hex = true;
-                }
-            }
-            const bool lex = (m.hl_exist >> h) & 1u;
-            const float lv = cst[kBandTailA + h] + mu;
-            const uint32_t flag = !lex ? (hex ? 0u : 3u) : !hex ? 1u : hv < lv ? 0u : lv < hv ? 1u : 2u;
-            rec2[h] = (flag << 30) | hcol;
-            tgt[h] = lv;
-            need |= m.hvalid[h] && (flag == 1u || flag == 2u);
+            tgt[h] = ca[h] + mu;
+            need |= m.hvalid[h] && ((m.hl_exist >> h) & 1u) && vh[h] == tgt[h];
         }
-        if (wave == 0 && lane == 0)
-            *reinterpret_cast<uint2*>(prec + (size_t)(obs - 1) * 4) = make_uint2(rec2[0], rec2[1]);
+        if (wave == 0 && lane == 0) {
+            float* r = reinterpret_cast<float*>(hring + ((obs - 1) & (kPathRing - 1)) * kRecWords);
+            r[0] = vo[0];
+            r[1] = vo[1];
+            r[2] = mu;
+        }
         return uniform((int)need) != 0;
     };
-    // j* candidates of this thread: the lowest own light row with fl(c_A + vp[s]) == target.
-    auto jstar_cands = [&](const HeavyConst& hc, const float (&tgt)[HM], uint32_t (&c)[HM]) {
+    // j* candidates of this thread: the lowest own light position with fl(c_A + vk[s]) == target,
+    // vk = the kept light scores of the record row's observation.
+    auto jstar_cands = [&](const HeavyConst& hc, const float (&tgt)[HM], uint32_t (&c)[HM], uint32_t parity) {
+        float vk[SM];
+#pragma unroll
+        for (int s = 0; s < SM; ++s) vk[s] = vkeep[parity * (SM * B) + s * B + t];
+        // positions made here (opaque base): hoisted out of the loop they would be spilled
+        uint32_t p0 = pos0;
+        asm volatile("" : "+v"(p0));
         const float ca[2] = {hc.c0.x, hc.c0.y};  // cst[kBandTailA + h]
 #pragma unroll
         for (int h = 0; h < HM; ++h) {
             uint32_t x = ~0u;
 #pragma unroll
-            for (int s = SM - 1; s >= 0; --s) x = (ca[h] + vp[s] == tgt[h]) ? plr[s] : x;
+            for (int s = SM - 1; s >= 0; --s) x = (ca[h] + vk[s] == tgt[h]) ? p0 + s : x;
             c[h] = x;
         }
     };
     static_assert(kBandTailA == 0 && kBandHeavy == 2, "jstar_cands reads cst[kBandTailA + h] from c0.xy");
 
+    // Flushes of the staging rings (global layouts: kernels.h, FusedBatch::cmask / hrec).
+    auto flush_masks = [&](uint32_t row0) {  // this wave's 32 rows from row0 (a multiple of 32)
+        const uint32_t* src = mring + (wave * kPathRing + (row0 & (kPathRing - 1))) * (2 * SM);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(b.cmask + b.cmask_off[q]) +
+                        ((size_t)(row0 >> 5) * W + wave) * (32 * 2 * SM);
+#pragma unroll
+        for (int k = 0; k < SM; ++k) dst[k * 64 + lane] = src[k * 64 + lane];
+    };
+    auto flush_recs = [&](uint32_t row0, uint32_t rows) {  // wave 0: rows row0 .. row0+rows-1
+        uint32_t* dst = b.hrec + b.hrec_off[q] + (size_t)row0 * kRecWords;
+        for (uint32_t x = lane; x < rows * kRecWords; x += 64)
+            dst[x] = hring[((row0 + x / kRecWords) & (kPathRing - 1)) * kRecWords + x % kRecWords];
+    };
+    uint32_t jpend[HM] = {~0u, ~0u};     // PATHS: j* candidates waiting for the next publish
     float own_p1 = kInf, own_p2 = kInf;  // W == 1: partials of the last two observations
     uint32_t pc_next = 0;                 // W > 1: count and cell of the observation before the
     float pm_next = kInf;                 // current one, read half a step before they are needed
@@ -534,31 +560,13 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
             if (lagged) asm volatile("" : "+v"(pmv), "+v"(pcv));
         }
         mark(1);
-        uint32_t jc[HM] = {~0u, ~0u};  // PATHS: j* candidates of record row i-2
-        uint64_t jword = ~0ull;        // PATHS, wave 0: j* cells of record row i-4
-        bool jvalid = false;
+        float mu = kInf, vo[HM];  // PATHS: light minimum and heavy scores of i-2
         if (lagged) {  // heavy scores of i-1
-            const float mu = W > 1 ? take_mu(i - 2, s2, pcv, pmv) : own_p2;
+            mu = W > 1 ? take_mu(i - 2, s2, pcv, pmv) : own_p2;
             if constexpr (PATHS) {
-                float tgt[HM];
-                if (heavy_paths(i - 1, mu, hc_prev, tgt)) jstar_cands(hc_prev, tgt, jc);
-                if constexpr (W > 1) {
-                    // every row's candidates of i-2 arrived with its count (take_mu above)
-                    if (wave == 0 && i >= 4) {
-                        jword = lds_load64(reinterpret_cast<const uint64_t*>(jcell + 2 * s2));
-                        jvalid = true;
-                    }
-                } else {
 #pragma unroll
-                    for (int h = 0; h < HM; ++h) {
-                        const uint32_t r = row_min16_u32(jc[h]);
-                        const uint32_t a = min((uint32_t)__builtin_amdgcn_readlane((int)r, 15),
-                                               (uint32_t)__builtin_amdgcn_readlane((int)r, 31));
-                        const uint32_t c = min((uint32_t)__builtin_amdgcn_readlane((int)r, 47),
-                                               (uint32_t)__builtin_amdgcn_readlane((int)r, 63));
-                        if (lane == 0) prec[(size_t)(i - 2) * 4 + 2 + h] = min(a, c);
-                    }
-                }
+                for (int h = 0; h < HM; ++h) vo[h] = vh[h];
+
             }
             heavy_update(mu, hc_prev);
         }
@@ -578,32 +586,33 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         mark(3);
         pin(vn);  // the light scores first: the boundary word has had the most time to land
         // lane 0, slot 0: the chain predecessor is the left neighbour's last score of i-1
-        float xb0 = xb[0];
+        float xb0 = 0.0f;
         {
             const float bv = take_bnd(i - 1, s1, bwv);
             float r = (e[0] + bw[0]) + bv;
-            if constexpr (PATHS) xb0 = lane == 0 ? r : xb0;
+            if constexpr (PATHS) xb0 = lane == 0 ? r : xb[0];
 #pragma unroll
             for (int h = 0; h < HA; ++h) r = fminf(r, xa[h][0] + vh[h]);
             vn[0] = lane == 0 ? r : vn[0];
         }
-        if constexpr (PATHS) {  // light masks of observation i (record row i-1), staged in lanes
+        if constexpr (PATHS) {  // light masks of observation i (record row i-1), staged lane by lane
             constexpr uint32_t L0 = ((s0 + kRing - 1) & 3u) * (2 * SM);
             auto mask_slot = [&](auto sc) {
                 constexpr int s = decltype(sc)::value;
                 const float xh = xa[0][s] + vh[0];
                 const float xbe = s == 0 ? xb0 : xb[s];
+                // heavy term taken: below the chain term, or tied and winning the tie
                 const uint64_t lt = __builtin_amdgcn_ballot_w64(xh < xbe);
                 const uint64_t eq = __builtin_amdgcn_ballot_w64(xh == xbe);
-                const uint64_t code = pmA[s] | (pmB[s] & lt) | (pmC[s] & eq);
+                const uint64_t code = mask_code(lt, eq, pmC[s]);
                 writelane<L0 + 2 * s>(pstage, (uint32_t)code);
                 writelane<L0 + 2 * s + 1>(pstage, (uint32_t)(code >> 32));
             };
             StaticFor<0, SM>::run(mask_slot);
         }
         if constexpr (W > 1) {
-            if constexpr (PATHS)
-                publish(slotc, i, row_partial(vn), vn[SM - 1], row_min16_u32(jc[0]), row_min16_u32(jc[1]));
+            if constexpr (PATHS)  // with the j* candidates found during step i-1
+                publish(slotc, i, row_partial(vn), vn[SM - 1], row_min16_u32(jpend[0]), row_min16_u32(jpend[1]));
             else
                 publish(slotc, i, row_partial(vn), vn[SM - 1]);
         } else {  // one wave: its own partials are the only ones, keep the last two in registers
@@ -612,12 +621,42 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         }
         mark(4);
         if constexpr (PATHS) {
+            // light masks of observation i (record row i-1) were staged before the publish
             if constexpr ((s0 & 3u) == 0) {  // rows i-4 .. i-1 staged: one store per wave
-                if (lane < 8 * SM) pmask[((size_t)((i - 1) >> 2) * W + wave) * (8 * SM) + lane] = pstage;
+                if (lane < 8 * SM) mring[(wave * kPathRing + ((i - 4) & (kPathRing - 1))) * (2 * SM) + lane] = pstage;
+                if constexpr (s0 == 0) {
+                    if ((i & 31u) == 0) flush_masks(i - 32);  // rows i-32 .. i-1 are in the ring
+                }
             }
-            if (jvalid && lane == 0) *reinterpret_cast<uint64_t*>(prec + (size_t)(i - 4) * 4 + 2) = jword;
+            // heavy records of observation i-1 (row i-2) and, when needed, its j* candidates
+            jpend[0] = ~0u;
+            jpend[1] = ~0u;
+            if (lagged) {
+                float tgt[HM];
+                if (heavy_record(i - 1, mu, hc_prev, vo, tgt)) jstar_cands(hc_prev, tgt, jpend, i & 1u);
+                if constexpr (W == 1) {  // one wave: reduce and store now
 #pragma unroll
-            for (int s = 0; s < SM; ++s) vp[s] = v[s];
+                    for (int h = 0; h < HM; ++h) {
+                        const uint32_t r = row_min16_u32(jpend[h]);
+                        const uint32_t a = min((uint32_t)__builtin_amdgcn_readlane((int)r, 15),
+                                               (uint32_t)__builtin_amdgcn_readlane((int)r, 31));
+                        const uint32_t c = min((uint32_t)__builtin_amdgcn_readlane((int)r, 47),
+                                               (uint32_t)__builtin_amdgcn_readlane((int)r, 63));
+                        if (lane == 0) hring[((i - 2) & (kPathRing - 1)) * kRecWords + kRecJ + h] = min(a, c);
+                    }
+                }
+            }
+            if (W > 1 && wave == 0 && i >= 5) {
+                // j* of record row i-5: every row's candidates, published with i-2, arrived with
+                // its count (take_mu above)
+                const uint64_t jw = lds_load64(reinterpret_cast<const uint64_t*>(jcell + 2 * s2));
+                if (lane == 0) *reinterpret_cast<uint64_t*>(hring + ((i - 5) & (kPathRing - 1)) * kRecWords + kRecJ) = jw;
+            }
+            if constexpr (s0 == 0) {
+                if (wave == 0 && (i & 31u) == 8 && i >= 40) flush_recs(i - 40, 32);  // rows complete
+            }
+#pragma unroll
+            for (int s = 0; s < SM; ++s) vkeep[(i & 1u) * (SM * B) + s * B + t] = vn[s];  // after the j* read
         }
 #pragma unroll
         for (int s = 0; s < SM; ++s) v[s] = vn[s];
@@ -715,35 +754,54 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         float mu = own_p2;
         if constexpr (W > 1) mu = take_mu(len - 2, sl, pc_next, pm_next);
         if constexpr (PATHS) {  // record row len-2: its j* straight from the kept scores v_{len-2}
-            float tgt[HM];
+            float tgt[HM], vo[HM];
             uint32_t jc[HM] = {~0u, ~0u};
-            if (heavy_paths(len - 1, mu, hc, tgt)) jstar_cands(hc, tgt, jc);
 #pragma unroll
-            for (int h = 0; h < HM; ++h) {
-                const uint32_t r = row_min16_u32(jc[h]);
-                if ((lane & 15u) == 15u)
+            for (int h = 0; h < HM; ++h) vo[h] = vh[h];
+            heavy_update(mu, hc);  // heavy_record's need compares the new heavy scores
+            if (heavy_record(len - 1, mu, hc, vo, tgt)) jstar_cands(hc, tgt, jc, len & 1u);
+#pragma unroll
+            for (int h = 0; h < HM; ++h) {  // jfin[h]: row len-2, jfin[2+h]: row len-3 (pending)
+                const uint32_t r = row_min16_u32(jc[h]), rp = row_min16_u32(jpend[h]);
+                if ((lane & 15u) == 15u) {
                     __hip_atomic_fetch_min(jfin + h, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_min(jfin + 2 + h, rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             }
+        } else {
+            heavy_update(mu, hc);
         }
-        heavy_update(mu, hc);
     }
     if constexpr (PATHS) {
         if (len > 1 && ((len - 1) & 3u) != 0 && lane < 8 * SM)  // the last, partial block of masks
-            pmask[((size_t)((len - 2) >> 2) * W + wave) * (8 * SM) + lane] = pstage;
+            mring[(wave * kPathRing + (((len - 2) & ~3u) & (kPathRing - 1))) * (2 * SM) + lane] = pstage;
         __syncthreads();  // every wave's j* candidates are in
-        if (wave == 0 && lane == 0 && len > 1) {  // rows the loop did not store (W > 1: len-4, len-3)
-            uint32_t* rr = prec + (size_t)(len - 2) * 4 + 2;
-            rr[0] = jfin[0];
-            rr[1] = jfin[1];
-            if (W > 1 && len >= 3) {
-                const uint32_t* c = jcell + 2 * ((len - 1) & (kRing - 1));
-                prec[(size_t)(len - 3) * 4 + 2] = c[0];
-                prec[(size_t)(len - 3) * 4 + 3] = c[1];
+        if (len > 1) {
+            // masks not flushed by the loop (it flushed rows below the last multiple of 32 <= len-1)
+            const uint32_t mdone = (len - 1) & ~31u;
+            if (mdone < len - 1) {
+                const uint32_t* src = mring + (wave * kPathRing + (mdone & (kPathRing - 1))) * (2 * SM);
+                uint32_t* dst = reinterpret_cast<uint32_t*>(b.cmask + b.cmask_off[q]) +
+                                ((size_t)(mdone >> 5) * W + wave) * (32 * 2 * SM);
+                const uint32_t cnt = (len - 1 - mdone) * 2 * SM;
+                for (uint32_t x = lane; x < cnt; x += 64) dst[x] = src[x];
             }
-            if (W > 1 && len >= 4) {
-                const uint32_t* c = jcell + 2 * ((len - 2) & (kRing - 1));
-                prec[(size_t)(len - 4) * 4 + 2] = c[0];
-                prec[(size_t)(len - 4) * 4 + 3] = c[1];
+            if (wave == 0) {
+                if (lane == 0) {
+                    // j* of rows the loop did not finish: len-2 (jfin), and with W > 1 len-3
+                    // (pending candidates), len-4 and len-5 (published with observations len-1, len-2)
+                    auto put = [&](uint32_t row, const uint32_t* c) {
+                        hring[(row & (kPathRing - 1)) * kRecWords + kRecJ] = c[0];
+                        hring[(row & (kPathRing - 1)) * kRecWords + kRecJ + 1] = c[1];
+                    };
+                    put(len - 2, jfin);
+                    if (W > 1 && len >= 3) put(len - 3, jfin + 2);
+                    if (W > 1 && len >= 4) put(len - 4, jcell + 2 * ((len - 1) & (kRing - 1)));
+                    if (W > 1 && len >= 5) put(len - 5, jcell + 2 * ((len - 2) & (kRing - 1)));
+                }
+                // records not flushed by the loop (it flushed rows below i-8 at i = 8 mod 32, i >= 40)
+                const uint32_t hdone = len - 1 >= 40 ? ((len - 1 - 8) & ~31u) : 0u;
+                flush_recs(hdone, len - 1 - hdone);
             }
         }
     }

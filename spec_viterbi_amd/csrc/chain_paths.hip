@@ -43,6 +43,7 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
     const uint64_t* msk = b.cmask + b.cmask_off[q];
     const uint32_t* rec = b.hrec + b.hrec_off[q];
     int32_t* out = paths + path_off[q];
+    const uint8_t* sym = b.symbols + b.sym_off[q];
     const int64_t best = b.best[q];
     int32_t s = best < 0 ? -1 : (int32_t)best;
     if (lane == 0) out[len - 1] = s;
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
             if (valid && p >= 0) {
                 const uint32_t tt = (uint32_t)p / SM, ss = (uint32_t)p % SM;
                 const uint64_t word =
-                    msk[(((uint64_t)r >> 2) * W + tt / 64) * (4 * SM) + ((uint32_t)r & 3u) * SM + ss];
+                    msk[((((uint64_t)r >> 5) * W + tt / 64) * 32 + ((uint32_t)r & 31u)) * SM + ss];
                 const uint32_t f = m.pflags[ss * B + tt];
                 if ((word >> (tt & 63u)) & 1ull) {
                     pred = m.hrow[0];
@@ -73,10 +74,39 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
                 }
             }
         } else if (valid) {  // heavy run: self-loops of heavy row h
+            // The heavy row's lexicographic (value, row) argmin at observation r+1, re-evaluated
+            // from the recorded inputs with the kernel's float operations (heavy_update): the
+            // heavy-row terms fl(cX + vo[k]) and the light-set term fl(cA + mu), whose lowest row
+            // is the recorded j* (a light position).
             const uint32_t h = (uint32_t)(-1 - pos);
-            const uint32_t x = rec[(uint64_t)r * 4 + h], js = rec[(uint64_t)r * 4 + 2 + h];
-            const uint32_t flag = x >> 30, hcol = x & 0x3FFFFFFFu;
-            const uint32_t k = flag == 0 ? hcol : flag == 1 ? js : flag == 2 ? min(hcol, js) : 0xFFFFFFFFu;
+            const uint32_t* rw = rec + (uint64_t)r * kRecWords;
+            const float vo[2] = {__builtin_bit_cast(float, rw[0]), __builtin_bit_cast(float, rw[1])};
+            const float mu = __builtin_bit_cast(float, rw[2]);
+            const uint32_t o = sym[r + 1];
+            const float* tl = m.erows + (size_t)o * m.erow + (size_t)SM * B;  // heavy constants of o
+            float hv = kInf;
+            uint32_t hcol = 0xFFFFFFFFu;
+            bool hex = false;
+#pragma unroll
+            for (int k = 0; k < kBandHeavy; ++k) {
+                if ((m.hx_exist >> (h * kBandHeavy + k)) & 1u) {
+                    const float val = tl[kBandTailX + h * kBandHeavy + k] + vo[k];
+                    const uint32_t col = (uint32_t)m.hrow[k];
+                    const bool take = !hex || val < hv || (val == hv && col < hcol);
+                    hv = take ? val : hv;
+                    hcol = take ? col : hcol;
+                    hex = true;
+                }
+            }
+            uint32_t k = hex ? hcol : 0xFFFFFFFFu;
+            if ((m.hl_exist >> h) & 1u) {
+                const float lv = tl[kBandTailA + h] + mu;
+                if (!hex || !(hv < lv)) {  // the light set wins or ties: its lowest row j*
+                    const uint32_t jp = rw[kRecJ + h];
+                    const uint32_t js = m.lrow[(jp % SM) * B + jp / SM];
+                    k = !hex || lv < hv ? js : min(hcol, js);
+                }
+            }
             pred = k == 0xFFFFFFFFu ? -1 : (int32_t)k;
             cont = pred == s;
         }
@@ -123,7 +153,9 @@ hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStre
     BandModel mm = m;
     FusedBatch bb = b;
     void* args[] = {&mm, &bb};
-    return hipLaunchKernel(fn, dim3(b.nseq), dim3(m.B), args, chain_lds_bytes(), stream);
+    // decoded paths keep the light scores of two observations in LDS
+    const size_t lds = chain_lds_bytes() + (b.cmask ? chain_path_lds_bytes(m.B / 64, m.SM) : 0);
+    return hipLaunchKernel(fn, dim3(b.nseq), dim3(m.B), args, lds, stream);
 }
 
 }  // namespace svh

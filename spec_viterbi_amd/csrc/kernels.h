@@ -58,10 +58,11 @@ struct FusedBatch {
     const uint64_t* bp_off;    // [nseq] element offset of sequence q's (len-1) x n block
     // Chain-kernel decoded paths (chain.hip): per backpointer row r (observation r+1)
     //   cmask: one 64-bit lane mask per (wave, slot): bit = "light position took its heavy term";
-    //          layout [r/4][wave][r%4][slot] u64, blocks of four rows
-    //   hrec:  [r][4] u32: [h] = flag<<30 | row of the heavy-term argmin of heavy row h,
-    //          [2+h] = j*, the lowest light row achieving the light-set minimum of heavy row h
-    //          (flag 0: heavy term wins, 1: light set wins, 2: tie, 3: no term; see chain.hip)
+    //          layout [r/32][wave][r%32][slot] u64, blocks of 32 rows
+    //   hrec:  [r][kRecWords] u32: [0..1] the heavy scores of observation r (f32), [2] the light
+    //          minimum of observation r (f32), [kRecJ + h] = j*: the lowest light position whose
+    //          term achieves heavy row h's light-set minimum (written when that term won or tied);
+    //          the traceback re-evaluates the heavy rows' argmin from these (chain_paths.hip)
     uint64_t* cmask;
     const uint64_t* cmask_off;  // [nseq] u64 offset of sequence q's masks
     uint32_t* hrec;
@@ -120,12 +121,12 @@ constexpr int kChainMaxSym = 32;
 constexpr int kChainMaxThreads = 512;
 constexpr uint32_t kChainSymChunk = 32768;  // symbols staged in LDS per refill
 constexpr int kChainRing = 8;  // exchange ring depth (observations in flight between waves)
-inline size_t chain_lds_bytes() {
+inline size_t chain_lds_bytes(size_t kept_floats = 0) {
     // heavy constants | tagged records [ring][waves][2] u64 | cells, counts, junk [ring] 4 B each |
     // reduction | path cells: j* [ring][2], final [2] + pad, junk [16] (u32) | staged symbols
     return (size_t)kChainMaxSym * kBandTail * sizeof(float) + (size_t)kChainRing * 2 * kMaxWaves * 8 +
            3 * kChainRing * 4 + 2 * kMaxWaves * sizeof(float) + (2 * kChainRing + 4 + 16) * 4 +
-           kChainSymChunk;
+           kChainSymChunk + kept_floats * sizeof(float);
 }
 // Chain kernel for (SM slots, W waves, HA heavy feeders, E streamed?); false if not instantiated.
 bool chain_supported(int sm, int waves, int ha, bool ge);
@@ -138,9 +139,16 @@ hipError_t launch_chain_traceback(const BandModel& m, const FusedBatch& b, const
                                   int32_t* paths, hipStream_t stream);
 // u64 masks / u32 records the decoded-path variant writes for a sequence of length len.
 inline uint64_t chain_mask_words(uint64_t len, uint32_t waves, uint32_t sm) {
-    return len > 1 ? (len - 1 + 3) / 4 * 4 * (uint64_t)waves * sm : 0;
+    return len > 1 ? (len - 1 + 31) / 32 * 32 * (uint64_t)waves * sm : 0;
 }
-inline uint64_t chain_hrec_words(uint64_t len) { return len > 1 ? (len - 1) * 4 : 0; }
+// Decoded-path staging in LDS: ring depth (rows) and bytes beyond chain_lds_bytes(): the kept
+// scores of two observations, the mask ring and the heavy-record ring.
+constexpr uint32_t kPathRing = 64;
+inline size_t chain_path_lds_bytes(uint32_t waves, uint32_t sm) {
+    return (size_t)2 * sm * 64 * waves * 4 + (size_t)waves * kPathRing * sm * 8 + (size_t)kPathRing * 8 * 4;
+}
+constexpr uint32_t kRecWords = 8, kRecJ = 4;
+inline uint64_t chain_hrec_words(uint64_t len) { return len > 1 ? (len - 1) * kRecWords : 0; }
 
 // CSR of T^T used by the generic kernel and the _spec precompute.
 struct CsrModel {
