@@ -134,6 +134,37 @@ int svh_batch_device_results(svh_batch_t b, float** scores, int64_t** best_state
 int svh_batch_elapsed_ms(svh_batch_t b, float* ms);
 int svh_batch_destroy(svh_batch_t b);
 
+/* Batch from uint8 symbols (the device format; e.g. straight from svh_reader_next). */
+int svh_batch_create_u8(svh_model_t m, uint64_t nseq, const uint64_t* offsets,
+                        const uint8_t* symbols, uint32_t flags, svh_batch_t* out);
+
+/* ---- streaming ingestion (the input side of the path) ------------------ */
+/* .ess: read_emit_seq semantics (data_reader.cpp:93-134).  FASTA: fasta_to_ess.py semantics
+ * (ess_files/fasta_to_ess.py:3-45): residues ACDEFGHIKLMNPQRSTVWY -> 0..19, X -> 0, lines
+ * stripped, '>' starts a sequence, an empty line or another residue is an error.  AUTO: by
+ * extension (.fasta/.fa/.faa/.fas, .ess), else by a leading '>'. */
+enum { SVH_FORMAT_AUTO = 0, SVH_FORMAT_ESS = 1, SVH_FORMAT_FASTA = 2 };
+typedef struct svh_reader* svh_reader_t;
+int svh_reader_open(const char* path, int format, svh_reader_t* out);
+/* The next chunk of whole sequences: at most max_seqs and at most max_symbols symbols in total
+ * (a single longer sequence comes alone).  *nseq == 0 at the end.  offsets (nseq + 1, from 0) and
+ * symbols point into reader-owned memory valid until the next call. */
+int svh_reader_next(svh_reader_t r, uint64_t max_seqs, uint64_t max_symbols, uint64_t* nseq,
+                    const uint64_t** offsets, const uint8_t** symbols);
+void svh_reader_close(svh_reader_t r);
+
+/* Results of one chunk of svh_decode_file (host memory valid during the call; paths NULL
+ * unless SVH_BATCH_PATHS).  Return non-zero to stop. */
+typedef int (*svh_result_fn)(void* user, uint64_t first_seq, uint64_t nseq, const uint64_t* offsets,
+                             const float* scores, const int64_t* best_state, const int32_t* paths);
+/* Decode a whole file chunk by chunk (chunks as svh_reader_next): parsing runs on a host thread
+ * ahead of the GPU, chunk k's kernels overlap chunk k-1's result copies and hand-off, in file
+ * order on the calling thread.  *nseq_total (nullable) = sequences decoded.  On a parse error the
+ * chunks before it have been delivered. */
+int svh_decode_file(svh_model_t m, const char* path, int format, uint32_t level, uint32_t flags,
+                    uint64_t max_seqs, uint64_t max_symbols, svh_result_fn fn, void* user,
+                    uint64_t* nseq_total);
+
 /* ---- one-shot convenience: upload, run, download --------------------------------------- */
 int svh_viterbi(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* offsets,
                 const uint64_t* symbols, float* scores, int64_t* best_state, int32_t* paths);

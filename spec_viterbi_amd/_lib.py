@@ -80,7 +80,19 @@ SIGNATURES = {
     "svh_batch_elapsed_ms": (c_int, [c_void_p, P_f32]),
     "svh_batch_destroy": (c_int, [c_void_p]),
     "svh_viterbi": (c_int, [c_void_p, c_uint32, c_uint64, P_u64, P_u64, P_f32, P_i64, P_i32]),
+    "svh_batch_create_u8": (c_int, [c_void_p, c_uint64, P_u64, POINTER(ctypes.c_uint8), c_uint32, POINTER(c_void_p)]),
+    "svh_reader_open": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
+    "svh_reader_next": (c_int, [c_void_p, c_uint64, c_uint64, P_u64, POINTER(P_u64),
+                                POINTER(POINTER(ctypes.c_uint8))]),
+    "svh_reader_close": (None, [c_void_p]),
+    "svh_decode_file": (c_int, [c_void_p, c_char_p, c_int, c_uint32, c_uint32, c_uint64, c_uint64, c_void_p,
+                                c_void_p, P_u64]),
 }
+
+SVH_FORMAT_AUTO, SVH_FORMAT_ESS, SVH_FORMAT_FASTA = 0, 1, 2
+# int (*svh_result_fn)(void*, uint64 first, uint64 nseq, const uint64* offsets, const float* scores,
+#                      const int64* best, const int32* paths)
+RESULT_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_uint64, c_uint64, P_u64, P_f32, P_i64, P_i32)
 
 
 def _load():

@@ -65,6 +65,13 @@ void DeviceBuffer::alloc(size_t nbytes) {
     hip_check(hipMalloc(&ptr, nbytes), "hipMalloc");
     bytes = nbytes;
 }
+void DeviceBuffer::reserve(size_t nbytes) {
+    if (!ptr || nbytes > bytes) alloc(nbytes);
+}
+void DeviceBuffer::upload_async(const void* src, size_t nbytes, hipStream_t s) {
+    reserve(nbytes);
+    if (nbytes) hip_check(hipMemcpyAsync(ptr, src, nbytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+}
 void DeviceBuffer::upload(const void* src, size_t nbytes, hipStream_t s) {
     alloc(nbytes);
     if (nbytes) hip_check(hipMemcpyAsync(ptr, src, nbytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
@@ -787,21 +794,47 @@ svh_model_info Model::info() const {
 // ------------------------------------------------------------------------------------------
 // Batches
 // ------------------------------------------------------------------------------------------
-Batch::Batch(Model* m, uint64_t nseq_, const uint64_t* offs, const uint64_t* symbols,
-             uint32_t flags)
+Batch::Batch(Model* m, uint64_t nseq_, const uint64_t* offs, const uint64_t* symbols, uint32_t flags)
     : model(m) {
+    init(flags);
+    load(nseq_, offs, symbols, nullptr, m->stream);
+    hip_check(hipStreamSynchronize(m->stream), "batch upload");
+}
+
+Batch::Batch(Model* m, uint64_t nseq_, const uint64_t* offs, const uint8_t* symbols, uint32_t flags)
+    : model(m) {
+    init(flags);
+    load(nseq_, offs, nullptr, symbols, m->stream);
+    hip_check(hipStreamSynchronize(m->stream), "batch upload");
+}
+
+void Batch::init(uint32_t flags) {
+    paths = (flags & SVH_BATCH_PATHS) != 0;
+    chain_paths = paths && model->band_for(true) != nullptr;
+    if (paths && !chain_paths && model->host.n >= kNoPred)
+        throw Error(SVH_E_UNSUPPORTED, "paths need states_num < 65535 for models the chain kernel does not cover");
+    DeviceGuard g(model->device);
+    hip_check(hipEventCreate(&ev_start), "hipEventCreate");
+    hip_check(hipEventCreate(&ev_stop), "hipEventCreate");
+}
+
+// (Re)load the batch's sequences: host packing, then asynchronous uploads on `s` into device
+// buffers that only ever grow (no hipFree / hipMalloc, hence no device-wide sync, once sized).
+// The host staging arrays are members, so they outlive the copies until the next load.
+void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, const uint8_t* sym8,
+                 hipStream_t s) {
     if (nseq_ == 0) throw Error(SVH_E_INVALID, "empty batch");
     if (nseq_ > 0x7FFFFFFFull) throw Error(SVH_E_UNSUPPORTED, "too many sequences in one batch");
-    if (!offs || !symbols) throw Error(SVH_E_INVALID, "null offsets/symbols");
+    if (!offs || (!sym64 && !sym8)) throw Error(SVH_E_INVALID, "null offsets/symbols");
+    const DeviceBandPlan* cpl = chain_paths ? model->band_for(true) : nullptr;
     nseq = (uint32_t)nseq_;
-    paths = (flags & SVH_BATCH_PATHS) != 0;
-    const DeviceBandPlan* cpl = paths ? m->band_for(true) : nullptr;
-    chain_paths = cpl != nullptr;
-    if (paths && !chain_paths && m->host.n >= kNoPred)
-        throw Error(SVH_E_UNSUPPORTED, "paths need states_num < 65535 for models the chain kernel does not cover");
     offsets.assign(offs, offs + nseq + 1);
     lens.resize(nseq);
-    std::vector<uint64_t> symoff(nseq), bpoff(nseq), pathoff(nseq), cmoff(nseq), hroff(nseq);
+    h_symoff.resize(nseq);
+    h_pathoff.resize(nseq);
+    h_bpoff.resize(nseq);
+    h_cmoff.resize(nseq);
+    h_hroff.resize(nseq);
     uint64_t bytes = 0, bpn = 0, cmn = 0, hrn = 0;
     for (uint32_t q = 0; q < nseq; ++q) {
         if (offs[q + 1] < offs[q]) throw Error(SVH_E_INVALID, "offsets must be non-decreasing");
@@ -810,57 +843,55 @@ Batch::Batch(Model* m, uint64_t nseq_, const uint64_t* offs, const uint64_t* sym
             throw Error(SVH_E_INVALID, "empty observation sequence (reference: seq[0] is undefined)");
         if (len > 0xFFFFFF00ull) throw Error(SVH_E_UNSUPPORTED, "sequence too long");
         lens[q] = (uint32_t)len;
-        symoff[q] = bytes;
+        h_symoff[q] = bytes;
         bytes += ((len + kSymPad + 4 + 15) / 16) * 16;
-        if (chain_paths) {
-            cmoff[q] = cmn;
+        if (cpl) {
+            h_cmoff[q] = cmn;
             cmn += chain_mask_words(len, cpl->plan.B / 64, cpl->plan.SM);
-            hroff[q] = hrn;
+            h_hroff[q] = hrn;
             hrn += chain_hrec_words(len);
-        } else {
-            bpoff[q] = bpn;
-            bpn += (len - 1) * (uint64_t)m->host.n;
+        } else if (paths) {
+            h_bpoff[q] = bpn;
+            bpn += (len - 1) * (uint64_t)model->host.n;
         }
-        pathoff[q] = offs[q] - offs[0];
+        h_pathoff[q] = offs[q] - offs[0];
     }
     total = offs[nseq] - offs[0];
-    std::vector<uint8_t> packed(bytes, 0);
-    const uint64_t S = m->host.S;
+    h_sym.assign(bytes, 0);
+    const uint64_t S = model->host.S;
     for (uint32_t q = 0; q < nseq; ++q) {
-        const uint64_t* src = symbols + offs[q];
-        uint8_t* dstp = packed.data() + symoff[q];
+        uint8_t* dstp = h_sym.data() + h_symoff[q];
         for (uint32_t i = 0; i < lens[q]; ++i) {
-            if (src[i] >= S)
-                throw Error(SVH_E_RANGE, "symbol " + std::to_string(src[i]) + " out of range (emit_num " +
+            const uint64_t x = sym64 ? sym64[offs[q] + i] : sym8[offs[q] + i];
+            if (x >= S)
+                throw Error(SVH_E_RANGE, "symbol " + std::to_string(x) + " out of range (emit_num " +
                                              std::to_string(S) + ")");
-            dstp[i] = (uint8_t)src[i];
+            dstp[i] = (uint8_t)x;
         }
     }
-    DeviceGuard g(m->device);
-    hipStream_t s = m->stream;
-    d_sym.upload(packed.data(), packed.size(), s);
-    d_symoff.upload(symoff.data(), symoff.size() * 8, s);
-    std::vector<uint32_t> zeros(nseq, 0);
-    d_begin.upload(zeros.data(), zeros.size() * 4, s);
-    d_end.upload(lens.data(), lens.size() * 4, s);
-    d_scores.alloc((size_t)nseq * m->host.n * 4);
-    d_best.alloc((size_t)nseq * 8);
+    h_zero.assign(nseq, 0);
+    DeviceGuard g(model->device);
+    d_sym.upload_async(h_sym.data(), h_sym.size(), s);
+    d_symoff.upload_async(h_symoff.data(), (size_t)nseq * 8, s);
+    d_begin.upload_async(h_zero.data(), (size_t)nseq * 4, s);
+    d_end.upload_async(lens.data(), (size_t)nseq * 4, s);
+    d_scores.reserve((size_t)nseq * model->host.n * 4);
+    d_best.reserve((size_t)nseq * 8);
     if (paths && chain_paths) {
-        d_cmask.alloc((size_t)std::max<uint64_t>(cmn, 1) * 8);
-        d_cmaskoff.upload(cmoff.data(), cmoff.size() * 8, s);
-        d_hrec.alloc((size_t)std::max<uint64_t>(hrn, 4) * 4);
-        d_hrecoff.upload(hroff.data(), hroff.size() * 8, s);
+        d_cmask.reserve((size_t)std::max<uint64_t>(cmn, 1) * 8);
+        d_cmaskoff.upload_async(h_cmoff.data(), (size_t)nseq * 8, s);
+        d_hrec.reserve((size_t)std::max<uint64_t>(hrn, kRecWords) * 4);
+        d_hrecoff.upload_async(h_hroff.data(), (size_t)nseq * 8, s);
     } else if (paths) {
-        d_bp.alloc((size_t)std::max<uint64_t>(bpn, 1) * 2);
-        d_bpoff.upload(bpoff.data(), bpoff.size() * 8, s);
+        d_bp.reserve((size_t)std::max<uint64_t>(bpn, 1) * 2);
+        d_bpoff.upload_async(h_bpoff.data(), (size_t)nseq * 8, s);
     }
     if (paths) {
-        d_pathoff.upload(pathoff.data(), pathoff.size() * 8, s);
-        d_paths.alloc((size_t)total * 4);
+        d_pathoff.upload_async(h_pathoff.data(), (size_t)nseq * 8, s);
+        d_paths.reserve((size_t)std::max<uint64_t>(total, 1) * 4);
     }
-    hip_check(hipEventCreate(&ev_start), "hipEventCreate");
-    hip_check(hipEventCreate(&ev_stop), "hipEventCreate");
-    hip_check(hipStreamSynchronize(s), "batch upload");
+    spec_ready_level = 0;
+    ran = false;
 }
 
 Batch::~Batch() {
@@ -977,17 +1008,33 @@ void Batch::read(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out
     if (!ran) throw Error(SVH_E_STATE, "svh_batch_read before svh_batch_run");
     if (paths_out && !paths) throw Error(SVH_E_STATE, "batch was created without SVH_BATCH_PATHS");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-    if (model->band.plan.ok && model->band.view.fault) {
-        uint32_t fault = 0;
-        hip_check(hipMemcpy(&fault, model->band.view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
-        if (fault) throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
-    }
+    model->check_fault();
     if (scores)
         hip_check(hipMemcpy(scores, d_scores.ptr, (size_t)nseq * model->host.n * 4, hipMemcpyDeviceToHost),
                   "scores D2H");
     if (best) hip_check(hipMemcpy(best, d_best.ptr, (size_t)nseq * 8, hipMemcpyDeviceToHost), "best D2H");
     if (paths_out)
         hip_check(hipMemcpy(paths_out, d_paths.ptr, (size_t)total * 4, hipMemcpyDeviceToHost), "paths D2H");
+}
+
+void Batch::read_async(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out) {
+    DeviceGuard g(model->device);
+    if (!ran) throw Error(SVH_E_STATE, "read before run");
+    if (paths_out && !paths) throw Error(SVH_E_STATE, "batch was created without SVH_BATCH_PATHS");
+    if (scores)
+        hip_check(hipMemcpyAsync(scores, d_scores.ptr, (size_t)nseq * model->host.n * 4, hipMemcpyDeviceToHost, s),
+                  "scores D2H");
+    if (best) hip_check(hipMemcpyAsync(best, d_best.ptr, (size_t)nseq * 8, hipMemcpyDeviceToHost, s), "best D2H");
+    if (paths_out)
+        hip_check(hipMemcpyAsync(paths_out, d_paths.ptr, (size_t)total * 4, hipMemcpyDeviceToHost, s), "paths D2H");
+}
+
+void Model::check_fault() const {
+    if (band.plan.ok && band.view.fault) {
+        uint32_t fault = 0;
+        hip_check(hipMemcpy(&fault, band.view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
+        if (fault) throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
+    }
 }
 
 float Batch::elapsed_ms() {

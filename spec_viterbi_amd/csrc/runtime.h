@@ -41,6 +41,8 @@ struct DeviceBuffer {
     ~DeviceBuffer();
     void alloc(size_t nbytes);
     void upload(const void* src, size_t nbytes, hipStream_t s);
+    void reserve(size_t nbytes);  // grow-only (keeps the allocation when large enough)
+    void upload_async(const void* src, size_t nbytes, hipStream_t s);  // reserve + async copy
     template <class T> T* as() const { return static_cast<T*>(ptr); }
 };
 
@@ -147,6 +149,8 @@ struct Model {
     const DeviceBandPlan* band_for(bool paths) const;
     void spec_build(uint32_t level, hipStream_t s);
     svh_model_info info() const;
+    // throws if a chain-kernel bounded wait gave up since the model was created (synchronous)
+    void check_fault() const;
 };
 
 struct Batch {
@@ -167,11 +171,24 @@ struct Batch {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     bool ran = false;
 
+    // host staging of the last load (kept alive for the asynchronous uploads)
+    std::vector<uint8_t> h_sym;
+    std::vector<uint64_t> h_symoff, h_pathoff, h_bpoff, h_cmoff, h_hroff;
+    std::vector<uint32_t> h_zero;
+
     Batch(Model* m, uint64_t nseq, const uint64_t* offsets, const uint64_t* symbols, uint32_t flags);
+    Batch(Model* m, uint64_t nseq, const uint64_t* offsets, const uint8_t* symbols, uint32_t flags);
+    // replace the sequences (same flags); uploads are asynchronous on s
+    void load(uint64_t nseq, const uint64_t* offsets, const uint64_t* sym64, const uint8_t* sym8, hipStream_t s);
     ~Batch();
     void run(uint32_t level, hipStream_t s);
     void read(hipStream_t s, float* scores, int64_t* best, int32_t* paths);
     float elapsed_ms();
+    // enqueue result copies (any pointer may be NULL) on s without waiting
+    void read_async(hipStream_t s, float* scores, int64_t* best, int32_t* paths);
+
+  private:
+    void init(uint32_t flags);
 };
 
 }  // namespace svh

@@ -8,6 +8,7 @@
 #include "HMM.h"
 #include "data_reader.h"
 #include "runtime.h"
+#include "stream.h"
 #include "svh.h"
 
 struct svh_hmm {
@@ -22,6 +23,11 @@ struct svh_model {
 struct svh_batch {
     std::unique_ptr<svh::Batch> impl;
     svh_model* owner;
+};
+struct svh_reader {
+    std::unique_ptr<svh::SeqReader> impl;
+    std::vector<uint64_t> offsets;
+    std::vector<uint8_t> symbols;
 };
 
 namespace {
@@ -200,6 +206,18 @@ int svh_batch_create(svh_model_t m, uint64_t nseq, const uint64_t* offsets,
     });
 }
 
+int svh_batch_create_u8(svh_model_t m, uint64_t nseq, const uint64_t* offsets, const uint8_t* symbols,
+                        uint32_t flags, svh_batch_t* out) {
+    return guarded([&] {
+        require(m && out, "null argument");
+        *out = nullptr;
+        auto b = std::make_unique<svh_batch>();
+        b->owner = m;
+        b->impl = std::make_unique<svh::Batch>(m->impl.get(), nseq, offsets, symbols, flags);
+        *out = b.release();
+    });
+}
+
 int svh_batch_run(svh_batch_t b, uint32_t level, void* stream) {
     return guarded([&] {
         require(b != nullptr, "null batch");
@@ -241,6 +259,42 @@ int svh_viterbi(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* of
         svh::Batch b(m->impl.get(), nseq, offsets, symbols, paths ? SVH_BATCH_PATHS : 0u);
         b.run(level, nullptr);
         b.read(nullptr, scores, best_state, paths);
+    });
+}
+
+// ---- streaming ingestion -----------------------------------------------------------------
+int svh_reader_open(const char* path, int format, svh_reader_t* out) {
+    return guarded([&] {
+        require(path && out, "null argument");
+        *out = nullptr;
+        auto r = std::make_unique<svh_reader>();
+        r->impl = std::make_unique<svh::SeqReader>(path, format);
+        *out = r.release();
+    });
+}
+
+int svh_reader_next(svh_reader_t r, uint64_t max_seqs, uint64_t max_symbols, uint64_t* nseq,
+                    const uint64_t** offsets, const uint8_t** symbols) {
+    return guarded([&] {
+        require(r && nseq, "null argument");
+        *nseq = 0;
+        if (!r->impl->next(max_seqs, max_symbols, r->offsets, r->symbols)) r->offsets.assign(1, 0);
+        *nseq = r->offsets.size() - 1;
+        if (offsets) *offsets = r->offsets.data();
+        if (symbols) *symbols = r->symbols.data();
+    });
+}
+
+void svh_reader_close(svh_reader_t r) { delete r; }
+
+int svh_decode_file(svh_model_t m, const char* path, int format, uint32_t level, uint32_t flags,
+                    uint64_t max_seqs, uint64_t max_symbols, svh_result_fn fn, void* user,
+                    uint64_t* nseq_total) {
+    return guarded([&] {
+        require(m && path && fn, "null argument");
+        if (nseq_total) *nseq_total = 0;
+        const uint64_t n = svh::decode_file(m->impl.get(), path, format, level, flags, max_seqs, max_symbols, fn, user);
+        if (nseq_total) *nseq_total = n;
     });
 }
 
