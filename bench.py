@@ -208,7 +208,8 @@ def main():
                                                               else f"_spec level {args.level}"),
                 "states": n, "nnz": nnz, "sequences_per_gpu": len(seqs), "observations_per_gpu": steps_obs,
                 "state_updates_per_gpu": updates_per_rank, "level": args.level,
-                "kernel": ("fused+traceback" if args.paths else KERNEL_NAMES.get(info["kernel"], "?")),
+                "kernel": (KERNEL_NAMES.get(info["paths_kernel"], "?") + "+traceback" if args.paths
+                           else KERNEL_NAMES.get(info["kernel"], "?")),
                 "paths": bool(args.paths), "spec_prep_s": None if prep_s is None else round(prep_s, 4), "threads": info["threads"],
                 "slots": info["slots"], "heavy_rows": info["heavy_rows"], "heavy_uniform": info["heavy_uniform"],
                 "parallelism": f"sequence-sharded x{world} (one process per GPU, no collective)",
