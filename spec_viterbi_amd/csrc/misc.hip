@@ -173,6 +173,14 @@ __global__ __launch_bounds__(256) void spec_extend_kernel(CsrModel m, const floa
 
 // K4: one level-L chunk, dense (min,+) GEMV per sequence: v'[j] = min_m fl(H[key][j][m] + v[m]).
 // grid (row blocks of 16, nseq), 256 threads = 4 waves x 4 rows, float4 loads along the row.
+// One level-L chunk: v_dst[q][j] = min_m fl(H_key[j][m] + v_src[q][m]) (GraphBLAS_spec_impl.cpp:76).
+// HBM-bound: every sequence streams one dense n x pstride product per chunk.  A workgroup takes
+// kChunkRows rows (kChunkRowsPerWave per wave, interleaved so each lane keeps that many 16-byte
+// loads in flight) against v staged once in LDS; the product rows are read non-temporally (a
+// product is reused only at a random later chunk, long after L2 would have dropped it).
+constexpr int kChunkRowsPerWave = 8;
+constexpr int kChunkRows = 4 * kChunkRowsPerWave;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void spec_chunk_kernel(CsrModel m, const float* products,
                                                          SpecChunkBatch c, uint32_t pstride) {
     extern __shared__ __attribute__((aligned(16))) float sv[];
@@ -188,19 +196,30 @@ __global__ __launch_bounds__(256) void spec_chunk_kernel(CsrModel m, const float
     const float* Hk = products + key * (size_t)n * pstride;
     const uint32_t nvec = pstride / 4;
     const float4* v4 = reinterpret_cast<const float4*>(sv);
+    const uint32_t j0 = blockIdx.x * kChunkRows + wave * kChunkRowsPerWave;
+    const f32x4* rows[kChunkRowsPerWave];
+    float acc[kChunkRowsPerWave];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        const uint32_t j = blockIdx.x * 16 + wave * 4 + rr;
-        if (j >= n) break;
-        const float4* row = reinterpret_cast<const float4*>(Hk + (size_t)j * pstride);
-        float acc = kInf;
-        for (uint32_t x = lane; x < nvec; x += 64) {
-            const float4 h = row[x];
-            const float4 v = v4[x];
-            acc = fminf(acc, fminf(fminf(h.x + v.x, h.y + v.y), fminf(h.z + v.z, h.w + v.w)));
-        }
-        acc = wave_min63(acc);
-        if (lane == 63) c.v_dst[(size_t)q * n + j] = acc;
+    for (int r = 0; r < kChunkRowsPerWave; ++r) {
+        const uint32_t j = min(j0 + r, n - 1);  // rows past n repeat the last one (result dropped)
+        rows[r] = reinterpret_cast<const f32x4*>(Hk + (size_t)j * pstride);
+        acc[r] = kInf;
+    }
+    for (uint32_t x = lane; x < nvec; x += 64) {
+        f32x4 h[kChunkRowsPerWave];
+#pragma unroll
+        for (int r = 0; r < kChunkRowsPerWave; ++r) h[r] = __builtin_nontemporal_load(rows[r] + x);
+        const float4 v = v4[x];
+#pragma unroll
+        for (int r = 0; r < kChunkRowsPerWave; ++r)
+            acc[r] = fminf(acc[r], fminf(fminf(h[r].x + v.x, h[r].y + v.y), fminf(h[r].z + v.z, h[r].w + v.w)));
+    }
+#pragma unroll
+    for (int r = 0; r < kChunkRowsPerWave; r += 2) wave_min63x2(acc[r], acc[r + 1]);
+    if (lane == 63) {
+#pragma unroll
+        for (int r = 0; r < kChunkRowsPerWave; ++r)
+            if (j0 + r < n) c.v_dst[(size_t)q * n + j0 + r] = acc[r];
     }
 }
 
@@ -327,7 +346,7 @@ hipError_t launch_spec_extend(const CsrModel& m, const float* mfold, const float
 hipError_t launch_spec_chunk(const CsrModel& m, const float* products, const SpecChunkBatch& c,
                              uint32_t pstride, hipStream_t stream) {
     if (c.nseq == 0) return hipSuccess;
-    dim3 grid((m.n + 15) / 16, c.nseq);
+    dim3 grid((m.n + kChunkRows - 1) / kChunkRows, c.nseq);
     const size_t lds = (size_t)pstride * sizeof(float);
     const void* fn = reinterpret_cast<const void*>(&spec_chunk_kernel);
     hipError_t e = set_lds_limit(fn, lds);
