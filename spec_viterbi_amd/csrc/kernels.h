@@ -236,6 +236,22 @@ struct SpecChunkBatch {
 };
 hipError_t launch_spec_chunk(const CsrModel& m, const float* products, const SpecChunkBatch& c,
                              uint32_t pstride, hipStream_t stream);
+// Time-parallel helpers (timepar.hip; Batch::run_time_parallel).  Row index tables per active
+// segment r: probe run from the exact start (x), from the guess (g), guess segment end (e),
+// destination row (out), probe covered the whole segment (full: out = X).
+struct TpRows {
+    const uint32_t* x;
+    const uint32_t* g;
+    const uint32_t* e;
+    const uint32_t* out;
+    const uint32_t* full;
+};
+hipError_t launch_tp_copy_rows(const float* in, const uint32_t* irow, float* out, const uint32_t* orow,
+                               uint32_t rows, uint32_t n, hipStream_t s);
+hipError_t launch_tp_correct(const float* X, const float* G, const float* E1, const TpRows& rows, uint32_t count,
+                             float* out, uint32_t n, float tol, uint32_t* flag, hipStream_t s);
+hipError_t launch_tp_finish(const float* S, float* scores, int64_t* best, uint32_t nseq, uint32_t n, hipStream_t s);
+
 // v0[q][j] = fl(E[s0][j] + start[j]) for every sequence.
 hipError_t launch_first_step(const CsrModel& m, const uint8_t* symbols, const uint64_t* sym_off,
                              uint32_t nseq, float* v, hipStream_t stream);

@@ -928,24 +928,7 @@ void Batch::run(uint32_t level, hipStream_t s) {
         fb.bp = d_bp.as<uint16_t>();
         fb.bp_off = d_bpoff.as<uint64_t>();
     }
-    auto launch_step_kernel = [&](const FusedBatch& b, bool want_paths) {
-        const DevicePlan* dp = model->plan_for(want_paths);
-        const DeviceBandPlan* bpl = model->band_for(want_paths);
-        if (bpl) {
-            const int ha = (int)std::max<uint32_t>(bpl->plan.HA, 1);
-            if (bpl->plan.chain) hip_check(launch_chain(bpl->view, ha, b, s), "chain Viterbi kernel");
-            else hip_check(launch_band(bpl->view, ha, b, s), "band Viterbi kernel");
-            if (bpl->view.dbg & (4u | 128u)) {
-                hip_check(hipStreamSynchronize(s), "stamps");
-                bpl->report_stamps(b.nseq);
-            }
-        } else if (dp) {
-            hip_check(launch_fused(dp->view, b, dp->plan.family, want_paths, s), "fused Viterbi kernel");
-        } else {
-            const uint32_t threads = std::min<uint32_t>(1024, ((model->host.n + 63) / 64) * 64);
-            hip_check(launch_generic(csr, b, (int)threads, want_paths, s), "generic Viterbi kernel");
-        }
-    };
+    auto launch_step_kernel = [&](const FusedBatch& b, bool want_paths) { model->launch_steps(b, want_paths, s); };
 
     hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
     if (level <= 1) {
@@ -1002,6 +985,192 @@ void Batch::run(uint32_t level, hipStream_t s) {
     ran = true;
 }
 
+// ------------------------------------------------------------------------------------------
+// Time-parallel run (opt-in, scores within rounding of the serial run).
+//   Sequence q of length L > 2*seg is cut into segments [b_k, e_k) of >= seg observations.
+//   1a  every segment k >= 1 runs its first `probe` observations from the guess (all zeros),
+//       segment 0 from the start column (exact) -> G
+//   1b  the rest of every segment continues from G -> E1 (all segments of all sequences at
+//       once: this is where the idle CUs go)
+//   2   for k = 1, 2, ...: segment k's probe from the exact start (the corrected end of k-1)
+//       -> X; if X - G is constant (within tol) the end is E1 + that constant, else the rest of
+//       the segment runs from X (exact; counted in *fallbacks)
+// The per-segment runs are ordinary step-kernel launches over a view of the batch (begin/end/
+// v_in per row); only the check/correction and the finish are kernels of their own.
+// ------------------------------------------------------------------------------------------
+void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream_t s, uint64_t* fallbacks) {
+    std::lock_guard<std::mutex> lock(model->mu);
+    DeviceGuard g(model->device);
+    if (!s) s = model->stream;
+    if (paths) throw Error(SVH_E_UNSUPPORTED, "time-parallel runs compute scores only (no decoded paths)");
+    if (seg < 2 || probe < 1 || probe >= seg)
+        throw Error(SVH_E_INVALID, "time-parallel run needs seg >= 2 and 1 <= probe < seg");
+    if (tol != tol) throw Error(SVH_E_INVALID, "tolerance is NaN");  // tol < 0: re-run every segment (exact)
+    const uint32_t n = model->host.n;
+    struct Seg {
+        uint32_t q, k, b, e;
+    };
+    std::vector<Seg> segs;
+    std::vector<uint32_t> nsegs(nseq), first_seg(nseq);
+    uint32_t kmax = 1;
+    for (uint32_t q = 0; q < nseq; ++q) {
+        const uint32_t L = lens[q];
+        const uint32_t P = L > 2 * seg ? L / seg : 1;  // segments of seg..2*seg-1 observations
+        first_seg[q] = (uint32_t)segs.size();
+        nsegs[q] = P;
+        kmax = std::max(kmax, P);
+        for (uint32_t k = 0; k < P; ++k) segs.push_back({q, k, k * seg, k + 1 == P ? L : (k + 1) * seg});
+    }
+    const uint32_t nv = (uint32_t)segs.size();
+    // device scratch (freed at return)
+    DeviceBuffer d_zero, d_G, d_E1, d_X, d_S, d_Y, d_vbest, d_flag;
+    DeviceBuffer d_vsym, d_vbeg, d_vend, d_vrow, d_rows;
+    std::vector<float> zero(n, 0.0f);
+    d_zero.upload_async(zero.data(), (size_t)n * 4, s);
+    d_G.reserve((size_t)nv * n * 4);
+    d_E1.reserve((size_t)nv * n * 4);
+    d_X.reserve((size_t)nv * n * 4);
+    d_S.reserve((size_t)nseq * n * 4);
+    d_Y.reserve((size_t)nv * n * 4);
+    d_vbest.reserve((size_t)nv * 8);
+    d_flag.reserve((size_t)nv * 4);
+    // one launch of the step kernel over rows (begin, end, v_in row) of the batch's sequences
+    std::vector<uint64_t> vsym;
+    std::vector<uint32_t> vbeg, vend, vrow;
+    auto launch_rows = [&](const float* v_in, float* out) {
+        const uint32_t rows = (uint32_t)vbeg.size();
+        if (rows == 0) return;
+        d_vsym.upload_async(vsym.data(), (size_t)rows * 8, s);
+        d_vbeg.upload_async(vbeg.data(), (size_t)rows * 4, s);
+        d_vend.upload_async(vend.data(), (size_t)rows * 4, s);
+        d_vrow.upload_async(vrow.data(), (size_t)rows * 4, s);
+        FusedBatch fb;
+        std::memset(&fb, 0, sizeof(fb));
+        fb.symbols = d_sym.as<uint8_t>();
+        fb.sym_off = d_vsym.as<uint64_t>();
+        fb.begin = d_vbeg.as<uint32_t>();
+        fb.end = d_vend.as<uint32_t>();
+        fb.v_in = v_in;
+        fb.v_in_row = d_vrow.as<uint32_t>();
+        fb.scores = out;
+        fb.best = d_vbest.as<int64_t>();
+        fb.nseq = rows;
+        model->launch_steps(fb, false, s);
+        // the host arrays are reused by the next launch: let this one's uploads land first
+        hip_check(hipStreamSynchronize(s), "time-parallel launch");
+    };
+    auto clear_rows = [&] {
+        vsym.clear();
+        vbeg.clear();
+        vend.clear();
+        vrow.clear();
+    };
+    hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
+    // 1a: probes from the guess (segment 0: from the start column)
+    clear_rows();
+    for (const Seg& x : segs) {
+        vsym.push_back(h_symoff[x.q]);
+        vbeg.push_back(x.k == 0 ? 0u : x.b);
+        vend.push_back(std::min(x.b + probe, x.e));
+        vrow.push_back(0);
+    }
+    launch_rows(d_zero.as<float>(), d_G.as<float>());
+    // 1b: the rest of every segment (a zero-step row copies its start)
+    clear_rows();
+    for (uint32_t v = 0; v < nv; ++v) {
+        const Seg& x = segs[v];
+        vsym.push_back(h_symoff[x.q]);
+        vbeg.push_back(std::min(x.b + probe, x.e));
+        vend.push_back(x.e);
+        vrow.push_back(v);
+    }
+    launch_rows(d_G.as<float>(), d_E1.as<float>());
+    // S[q] = end of segment 0 (exact)
+    {
+        std::vector<uint32_t> irow(nseq), orow(nseq);
+        for (uint32_t q = 0; q < nseq; ++q) {
+            irow[q] = first_seg[q];
+            orow[q] = q;
+        }
+        d_rows.upload_async(irow.data(), (size_t)nseq * 4, s);
+        DeviceBuffer d_orow;
+        d_orow.upload_async(orow.data(), (size_t)nseq * 4, s);
+        hip_check(launch_tp_copy_rows(d_E1.as<float>(), d_rows.as<uint32_t>(), d_S.as<float>(), d_orow.as<uint32_t>(),
+                                      nseq, n, s),
+                  "time-parallel copy");
+        hip_check(hipStreamSynchronize(s), "time-parallel copy");
+    }
+    // 2: segments 1, 2, ... in order, all sequences at once
+    uint64_t nfall = 0;
+    DeviceBuffer d_rx, d_rg, d_re, d_ro, d_rf;
+    for (uint32_t k = 1; k < kmax; ++k) {
+        std::vector<uint32_t> act;  // virtual segment ids of segment k
+        for (uint32_t q = 0; q < nseq; ++q)
+            if (nsegs[q] > k) act.push_back(first_seg[q] + k);
+        if (act.empty()) break;
+        const uint32_t na = (uint32_t)act.size();
+        // probe from the exact start S[q] -> X rows 0..na-1
+        clear_rows();
+        std::vector<uint32_t> rx(na), rg(na), re(na), ro(na), rf(na);
+        for (uint32_t a = 0; a < na; ++a) {
+            const Seg& x = segs[act[a]];
+            vsym.push_back(h_symoff[x.q]);
+            vbeg.push_back(x.b);
+            vend.push_back(std::min(x.b + probe, x.e));
+            vrow.push_back(x.q);
+            rx[a] = a;
+            rg[a] = act[a];
+            re[a] = act[a];
+            ro[a] = x.q;
+            rf[a] = x.b + probe >= x.e ? 1u : 0u;
+        }
+        launch_rows(d_S.as<float>(), d_X.as<float>());
+        d_rx.upload_async(rx.data(), (size_t)na * 4, s);
+        d_rg.upload_async(rg.data(), (size_t)na * 4, s);
+        d_re.upload_async(re.data(), (size_t)na * 4, s);
+        d_ro.upload_async(ro.data(), (size_t)na * 4, s);
+        d_rf.upload_async(rf.data(), (size_t)na * 4, s);
+        TpRows tr{d_rx.as<uint32_t>(), d_rg.as<uint32_t>(), d_re.as<uint32_t>(), d_ro.as<uint32_t>(),
+                  d_rf.as<uint32_t>()};
+        hip_check(launch_tp_correct(d_X.as<float>(), d_G.as<float>(), d_E1.as<float>(), tr, na, d_S.as<float>(), n,
+                                    tol, d_flag.as<uint32_t>(), s),
+                  "time-parallel correction");
+        std::vector<uint32_t> flag(na);
+        hip_check(hipMemcpyAsync(flag.data(), d_flag.ptr, (size_t)na * 4, hipMemcpyDeviceToHost, s), "flags D2H");
+        hip_check(hipStreamSynchronize(s), "time-parallel flags");
+        // not converged: the rest of the segment from X, exactly, into Y, then into S
+        clear_rows();
+        std::vector<uint32_t> yi, yo;
+        for (uint32_t a = 0; a < na; ++a) {
+            if (!flag[a]) continue;
+            const Seg& x = segs[act[a]];
+            vsym.push_back(h_symoff[x.q]);
+            vbeg.push_back(x.b + probe);
+            vend.push_back(x.e);
+            vrow.push_back(a);
+            yi.push_back((uint32_t)yi.size());
+            yo.push_back(x.q);
+        }
+        if (!yi.empty()) {
+            nfall += yi.size();
+            launch_rows(d_X.as<float>(), d_Y.as<float>());
+            d_rx.upload_async(yi.data(), yi.size() * 4, s);
+            d_ro.upload_async(yo.data(), yo.size() * 4, s);
+            hip_check(launch_tp_copy_rows(d_Y.as<float>(), d_rx.as<uint32_t>(), d_S.as<float>(), d_ro.as<uint32_t>(),
+                                          (uint32_t)yi.size(), n, s),
+                      "time-parallel copy");
+            hip_check(hipStreamSynchronize(s), "time-parallel fallback");
+        }
+    }
+    hip_check(launch_tp_finish(d_S.as<float>(), d_scores.as<float>(), d_best.as<int64_t>(), nseq, n, s),
+              "time-parallel finish");
+    hip_check(hipEventRecord(ev_stop, s), "hipEventRecord");
+    hip_check(hipStreamSynchronize(s), "time-parallel run");
+    model->check_fault();
+    if (fallbacks) *fallbacks = nfall;
+    ran = true;
+}
+
 void Batch::read(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out) {
     DeviceGuard g(model->device);
     if (!s) s = model->stream;
@@ -1027,6 +1196,26 @@ void Batch::read_async(hipStream_t s, float* scores, int64_t* best, int32_t* pat
     if (best) hip_check(hipMemcpyAsync(best, d_best.ptr, (size_t)nseq * 8, hipMemcpyDeviceToHost, s), "best D2H");
     if (paths_out)
         hip_check(hipMemcpyAsync(paths_out, d_paths.ptr, (size_t)total * 4, hipMemcpyDeviceToHost, s), "paths D2H");
+}
+
+// One pass of the per-observation step kernel over a batch view (steps begin..end-1 of each row).
+void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) const {
+    const DevicePlan* dp = plan_for(want_paths);
+    const DeviceBandPlan* bpl = band_for(want_paths);
+    if (bpl) {
+        const int ha = (int)std::max<uint32_t>(bpl->plan.HA, 1);
+        if (bpl->plan.chain) hip_check(launch_chain(bpl->view, ha, b, s), "chain Viterbi kernel");
+        else hip_check(launch_band(bpl->view, ha, b, s), "band Viterbi kernel");
+        if (bpl->view.dbg & (4u | 128u)) {
+            hip_check(hipStreamSynchronize(s), "stamps");
+            bpl->report_stamps(b.nseq);
+        }
+    } else if (dp) {
+        hip_check(launch_fused(dp->view, b, dp->plan.family, want_paths, s), "fused Viterbi kernel");
+    } else {
+        const uint32_t threads = std::min<uint32_t>(1024, ((host.n + 63) / 64) * 64);
+        hip_check(launch_generic(csr_view(), b, (int)threads, want_paths, s), "generic Viterbi kernel");
+    }
 }
 
 void Model::check_fault() const {

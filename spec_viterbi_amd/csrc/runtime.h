@@ -151,6 +151,8 @@ struct Model {
     svh_model_info info() const;
     // throws if a chain-kernel bounded wait gave up since the model was created (synchronous)
     void check_fault() const;
+    // one pass of the step kernel the model plans for (chain, band, fused or generic)
+    void launch_steps(const FusedBatch& b, bool paths, hipStream_t s) const;
 };
 
 struct Batch {
@@ -184,6 +186,9 @@ struct Batch {
     void run(uint32_t level, hipStream_t s);
     void read(hipStream_t s, float* scores, int64_t* best, int32_t* paths);
     float elapsed_ms();
+    // opt-in time-parallel scores (segments of >= seg observations, probes of `probe`; see
+    // runtime.cpp); synchronous; *fallbacks = segments that did not converge within the probe
+    void run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream_t s, uint64_t* fallbacks);
     // enqueue result copies (any pointer may be NULL) on s without waiting
     void read_async(hipStream_t s, float* scores, int64_t* best, int32_t* paths);
 

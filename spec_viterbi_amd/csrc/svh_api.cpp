@@ -225,6 +225,14 @@ int svh_batch_run(svh_batch_t b, uint32_t level, void* stream) {
     });
 }
 
+int svh_batch_run_time_parallel(svh_batch_t b, uint32_t seg_len, uint32_t probe_len, float rel_tol,
+                                void* stream, uint64_t* fallbacks) {
+    return guarded([&] {
+        require(b != nullptr, "null batch");
+        b->impl->run_time_parallel(seg_len, probe_len, rel_tol, static_cast<hipStream_t>(stream), fallbacks);
+    });
+}
+
 int svh_batch_read(svh_batch_t b, void* stream, float* scores, int64_t* best_state,
                    int32_t* paths) {
     return guarded([&] {

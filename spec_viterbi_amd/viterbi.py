@@ -102,6 +102,16 @@ class DeviceBatch:
     def run(self, level: int = 0, stream: int | None = None) -> None:
         _lib.check(_lib.lib.svh_batch_run(self._h, int(level), ctypes.c_void_p(stream or 0)))
 
+    def run_time_parallel(self, seg_len: int = 1024, probe_len: int = 256, rel_tol: float = 1e-6,
+                          stream: int | None = None) -> int:
+        """Opt-in time-parallel scores (svh_batch_run_time_parallel): long sequences are cut into
+        segments that run concurrently; scores match the serial pass up to rounding.  Returns the
+        number of segments that did not converge within the probe and were re-run exactly."""
+        fb = ctypes.c_uint64()
+        _lib.check(_lib.lib.svh_batch_run_time_parallel(self._h, int(seg_len), int(probe_len), float(rel_tol),
+                                                         ctypes.c_void_p(stream or 0), ctypes.byref(fb)))
+        return int(fb.value)
+
     def read(self, stream: int | None = None, want_paths: bool = False):
         scores = np.empty((self.nseq, self.model.n), np.float32)
         best = np.empty(self.nseq, np.int64)

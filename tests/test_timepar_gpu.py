@@ -1,0 +1,89 @@
+"""GPU: the opt-in time-parallel pass against the oracle.
+
+Not bit-exact by design (a converged segment's end is the guess run's end plus a constant), so
+the bar is the reference's own tolerance, HMM::almost_equal (|d| <= 1.0, Viterbi_impl/HMM.h:43-49),
+tightened here to a relative 1e-5; with rel_tol < 0 every segment is re-run and the result must be
+bit-exact (the orchestration itself is then checked exactly)."""
+import numpy as np
+import pytest
+
+import spec_viterbi_amd as svh
+from spec_viterbi_amd import _lib
+from oracle import oracle
+from tests.conftest import chmm, ess
+from tests.helpers import bit_equal, random_chain_hmm, random_hmm, random_seqs
+
+pytestmark = pytest.mark.gpu
+
+
+def close(a, b, rel=1e-5):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    fin = np.isfinite(b)
+    return bool(np.array_equal(np.isfinite(a), fin) and np.all(np.abs(a[fin] - b[fin]) <= rel * np.maximum(1.0, np.abs(b[fin]))))
+
+
+def test_forced_fallback_is_bit_exact():
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("covid-19.ess"))
+    model = svh.DeviceModel(hmm)
+    batch = model.batch(seqs)
+    fb = batch.run_time_parallel(seg_len=300, probe_len=40, rel_tol=-1.0)
+    assert fb > 0
+    scores, best = batch.read()
+    one_s, one_b = model.viterbi(seqs)
+    assert bit_equal(scores, one_s) and np.array_equal(best, one_b)
+
+
+@pytest.mark.parametrize("seg,probe", [(1024, 256), (512, 128), (2000, 500)])
+def test_covid_2405_within_tolerance(seg, probe):
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("covid-19.ess"))
+    model = svh.DeviceModel(hmm)
+    batch = model.batch(seqs)
+    fb = batch.run_time_parallel(seg_len=seg, probe_len=probe)
+    scores, best = batch.read()
+    for q, seq in enumerate(seqs):
+        ref = oracle.viterbi(hmm, seq)
+        assert close(scores[q], ref), (q, fb)
+        assert best[q] == int(np.argmin(ref)), q
+
+
+@pytest.mark.parametrize("L,seed", [(300, 1), (64, 2), (1000, 3)])
+def test_random_chain_models_within_tolerance(L, seed):
+    hmm = random_chain_hmm(L, seed=seed)
+    seqs = random_seqs(20, [5000, 3000, 1, 77, 2500], seed=seed)
+    model = svh.DeviceModel(hmm)
+    batch = model.batch(seqs)
+    batch.run_time_parallel(seg_len=700, probe_len=200)
+    scores, best = batch.read()
+    for q, seq in enumerate(seqs):
+        ref = oracle.viterbi(hmm, seq)
+        assert close(scores[q], ref), q
+
+
+def test_converges_on_a_mixing_model():
+    """Segments of an ergodic random model converge within the probe (rank convergence), so most
+    are not re-run -- and the scores stay within tolerance of the oracle."""
+    hmm = random_hmm(300, out_degree=4, seed=3)
+    seqs = random_seqs(hmm.emit_num, [8000, 6000, 4000, 100], seed=5)
+    model = svh.DeviceModel(hmm)
+    batch = model.batch(seqs)
+    fb = batch.run_time_parallel(seg_len=1024, probe_len=256)
+    assert fb <= 3  # of 12 segments after the first ones
+    scores, best = batch.read()
+    for q, seq in enumerate(seqs):
+        ref = oracle.viterbi(hmm, seq)
+        assert close(scores[q], ref), q
+        assert best[q] == int(np.argmin(ref)), q
+
+
+def test_errors():
+    hmm = svh.read_HMM(chmm("100.chmm"))
+    model = svh.DeviceModel(hmm)
+    seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    with pytest.raises(_lib.SvhError) as e:
+        model.batch(seqs, paths=True).run_time_parallel()
+    assert e.value.code == _lib.SVH_E_UNSUPPORTED
+    with pytest.raises(_lib.SvhError) as e:
+        model.batch(seqs).run_time_parallel(seg_len=100, probe_len=100)
+    assert e.value.code == _lib.SVH_E_INVALID
