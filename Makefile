@@ -16,11 +16,13 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) \
 HOSTFLAGS := --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall
 
 HIP_SRCS  := $(wildcard $(CSRC)/fused_*.hip) $(CSRC)/misc.hip $(CSRC)/band.hip $(wildcard $(CSRC)/chain_*.hip) $(CSRC)/timepar.hip
-HOST_SRCS := $(CSRC)/runtime.cpp $(CSRC)/svh_api.cpp $(CSRC)/HIP_impl.cpp $(CSRC)/data_reader.cpp $(CSRC)/stream.cpp
+HOST_SRCS := $(CSRC)/runtime.cpp $(CSRC)/svh_api.cpp $(CSRC)/HIP_impl.cpp $(CSRC)/data_reader.cpp $(CSRC)/stream.cpp \
+             $(CSRC)/seqreader.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS))
 HDRS := $(wildcard $(CSRC)/*.h) $(wildcard include/*.h)
 
-CPP_TESTS := tests/cpp/test_HIP_impl tests/cpp/test_HIP_spec_impl tests/cpp/test_semantic_equality
+CPP_TESTS := tests/cpp/test_HIP_impl tests/cpp/test_HIP_spec_impl tests/cpp/test_semantic_equality \
+             tests/cpp/test_readers_asan
 
 .PHONY: all lib oracle ref tests clean
 all: lib oracle tests ref
@@ -44,6 +46,13 @@ $(LIB): $(OBJS)
 # Oracle: plain C, every add rounded on its own (test infrastructure only).
 $(ORACLE): oracle/viterbi_oracle.c oracle/viterbi_oracle.h
 	$(CC) -O2 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -shared -o $@ oracle/viterbi_oracle.c
+
+# Host readers (the code that parses untrusted input) under AddressSanitizer + UBSan, without HIP:
+# the counterpart of the reference's valgrind memcheck run (run_tests.sh:4-7).
+tests/cpp/test_readers_asan: tests/cpp/test_readers_asan.cpp $(CSRC)/data_reader.cpp $(CSRC)/seqreader.cpp \
+		$(CSRC)/seqreader.h $(CSRC)/error.h include/data_reader.h include/HMM.h
+	$(CXX) -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -Iinclude -I$(CSRC) \
+		-o $@ tests/cpp/test_readers_asan.cpp $(CSRC)/data_reader.cpp $(CSRC)/seqreader.cpp
 
 # C++ tests written against the reference's interfaces (tests/cpp/*.cpp).
 tests/cpp/%: tests/cpp/%.cpp tests/cpp/test_helper.h $(LIB)

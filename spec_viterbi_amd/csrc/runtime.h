@@ -10,15 +10,12 @@
 #include <string>
 #include <vector>
 
+#include "error.h"
 #include "kernels.h"
 #include "svh.h"
 
 namespace svh {
 
-struct Error : std::runtime_error {
-    int code;
-    Error(int c, const std::string& msg) : std::runtime_error(msg), code(c) {}
-};
 
 void hip_check(hipError_t e, const char* what);
 
