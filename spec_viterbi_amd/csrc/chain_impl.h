@@ -145,48 +145,6 @@ struct StaticFor<N, N> {
     __device__ __forceinline__ static void run(F&) {}
 };
 
-// Unsigned row minimum (the lowest light row achieving a heavy row's light-set minimum).
-__device__ __forceinline__ uint32_t row_min16_u32(uint32_t x) {
-    asm("s_nop 1\n\t"
-        "v_min_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_min_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_min_u32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_min_u32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf"
-        : "+v"(x));
-    return x;
-}
-
-// publish_rows plus the decoded-path cells: wave 0 resets the two j* cells two observations
-// ahead (other waves hit junk words), every row adds its j* candidates (ds_min_u32) before the
-// arrival count, so a reader that sees every arrival of observation k sees every candidate.
-template <uint32_t RST_OFF, uint32_t CELL_OFF, uint32_t CNT_OFF, uint32_t BND_OFF, uint32_t JRST_OFF,
-          uint32_t JCELL_OFF>
-__device__ __forceinline__ void publish_rows_paths(uint32_t rbase, uint32_t cbase, float rowmin, uint32_t bbase,
-                                                   uint64_t bndv, float inf, uint32_t one, uint64_t lanes,
-                                                   uint32_t jrbase, uint32_t jcbase, uint32_t c0, uint32_t c1,
-                                                   uint64_t ones) {
-    uint64_t saved;
-    asm volatile(
-        "s_and_saveexec_b64 %0, %6\n\t"
-        "s_nop 1\n\t"
-        "ds_write_b32 %1, %7 offset:%13\n\t"
-        "ds_write_b64 %9, %12 offset:%17\n\t"
-        "ds_min_f32 %2, %3 offset:%14\n\t"
-        "ds_min_u32 %10, %11 offset:%18\n\t"
-        "ds_min_u32 %10, %19 offset:%20\n\t"
-        "ds_add_u32 %2, %8 offset:%15\n\t"
-        "ds_write_b64 %4, %5 offset:%16\n\t"
-        "s_mov_b64 exec, %0"
-        : "=&s"(saved)
-        : "v"(rbase), "v"(cbase), "v"(rowmin), "v"(bbase), "v"(bndv), "s"(lanes), "v"(inf), "v"(one),
-          "v"(jrbase), "v"(jcbase), "v"(c0), "v"(ones), "n"(RST_OFF), "n"(CELL_OFF), "n"(CNT_OFF),
-          "n"(BND_OFF), "n"(JRST_OFF), "n"(JCELL_OFF), "v"(c1), "n"(JCELL_OFF + 4)
-        : "memory", "scc");
-}
-
 __device__ __forceinline__ unsigned long long stamp() {
     unsigned long long x;
     __builtin_amdgcn_sched_barrier(0);
@@ -201,12 +159,12 @@ __device__ __forceinline__ unsigned long long stamp() {
 //   * light position p: its two candidates (position p-1, heavy row 0) are compared in every lane
 //     and one 64-bit lane mask per slot records "took the heavy term" (staged in a VGPR by
 //     v_writelane, stored every four observations);
-//   * heavy row h: the heavy-term argmin and the flag heavy / light / tie / none are decided from
-//     the heavy scores every thread holds (wave 0 stores them).  The light-set argmin j* = the
-//     lowest light position with fl(c + v[j]) == fl(c + min v) is a second pass over a kept copy
-//     of the light scores, run only when some flag needs it (rare: on 2405.chmm about 20 of
-//     3500 observations), reduced through two LDS min cells published with the next
-//     observation's exchange, before its arrival count.
+//   * heavy row h: its argmin is re-evaluated by the traceback from the heavy scores and the
+//     light minimum of the observation before (wave 0 records them).  Where the light-set term
+//     wins or ties, the traceback also needs j* = the lowest light position with
+//     fl(c + v[j]) == fl(c + min v): it recomputes that row's light scores from a checkpoint
+//     (every kCkptEvery-th row of light scores, stored here) instead of this kernel finding j*
+//     for every observation (on 2405.chmm the path needs it about once per sequence).
 template <int SM, int W, int HA, bool GE, bool STAMP = false, int DIAG = 0, bool PATHS = false>
 __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
     static_assert(!PATHS || (HA == 1 && !GE && !STAMP && DIAG == 0), "decoded paths: HA 1, E in VGPRs");
@@ -230,13 +188,7 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     uint32_t* pcnt = reinterpret_cast<uint32_t*>(pcell + kRing);
     float* junk = reinterpret_cast<float*>(pcnt + kRing);
     float* red = junk + kRing;
-    uint32_t* jcell = reinterpret_cast<uint32_t*>(red + 2 * kMaxWaves);  // [kRing][2] (8 B aligned)
-    uint32_t* jfin = jcell + 2 * kRing;                                 // [2] (+2 pad)
-    uint32_t* jjunk = jfin + 4;                                         // [16]
-    uint8_t* symr = reinterpret_cast<uint8_t*>(jjunk + 16);
-    // PATHS: the light scores of the last two observations, [i & 1][s * B + t] (each lane reads
-    // back only its own: a per-lane spill, no inter-wave order needed)
-    float* vkeep = reinterpret_cast<float*>(symr + kChainSymChunk);
+    uint8_t* symr = reinterpret_cast<uint8_t*>(red + 2 * kMaxWaves);  // 16 B aligned
 
     // ---- resident tables ---------------------------------------------------------------------
     // GE == false: et[s][o] = E[o][position t*SM+s] in VGPRs, picked by s_set_gpr_idx.
@@ -287,9 +239,6 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     if (t < kRing) {
         pcell[t] = kInf;
         pcnt[t] = 0;
-    }
-    if constexpr (PATHS) {
-        if (t < 2 * kRing + 4) jcell[t] = 0xFFFFFFFFu;  // jcell and jfin
     }
 
     // ---- sequence ----------------------------------------------------------------------------
@@ -369,21 +318,10 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         if constexpr (PUB1) return wave_min63(pm);  // diagnostic: lane 63 alone publishes
         return row_min16(pm);
     };
-    // decoded paths: j* cells (wave 0 resets them, other waves hit junk), all-ones reset value
-    uint32_t jcbase = lds_addr(jcell), jrbase = lds_addr(wave ? jjunk : jcell);
-    uint64_t ones64 = ~0ull;
-    if constexpr (PATHS) asm volatile("" : "+v"(jcbase), "+v"(jrbase), "+v"(ones64));
-    auto publish = [&](auto slotc, uint32_t obs, float rowmin, float vlast, uint32_t c0 = ~0u, uint32_t c1 = ~0u) {
+    auto publish = [&](auto slotc, uint32_t obs, float rowmin, float vlast) {
         constexpr uint32_t K = decltype(slotc)::value;
-        if constexpr (PATHS) {
-            publish_rows_paths<((K + 2) % kRing) * 4, K * 4, kCntOff + K * 4, K * kMaxWaves * 16,
-                               ((K + 2) % kRing) * 8, K * 8>(
-                rbase, cbase, rowmin, bbase, pack(obs + 1u, vlast), inf_v, one, 0x8000800080008000ull, jrbase,
-                jcbase, c0, c1, ones64);
-        } else {
-            publish_rows<((K + 2) % kRing) * 4, K * 4, kCntOff + K * 4, K * kMaxWaves * 16>(
-                rbase, cbase, rowmin, bbase, pack(obs + 1u, vlast), inf_v, one, PUB1 ? 0x8000000000000000ull : 0x8000800080008000ull);
-        }
+        publish_rows<((K + 2) % kRing) * 4, K * 4, kCntOff + K * 4, K * kMaxWaves * 16>(
+            rbase, cbase, rowmin, bbase, pack(obs + 1u, vlast), inf_v, one, PUB1 ? 0x8000000000000000ull : 0x8000800080008000ull);
     };
     // Arrivals the count of obs's slot has once every row published obs (obs >= first - 1).
     auto arrivals = [&](uint32_t obs) -> uint32_t { return (PUB1 ? 1u : 4u) * W * (((obs + 1u - first) / kRing) + 1u); };
@@ -451,66 +389,41 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     // a chain term xb = +inf, so the heavy term is taken.
     //
     // Output staging: nothing is stored to HBM inside the loop except one flush per 32
-    // observations.  The masks go to an LDS ring per wave (mring [wave][64 rows][SM] u64, four
-    // rows per ds_write), the heavy records to an LDS ring written by wave 0 (hring [64 rows][4]).
+    // observations and the checkpoint rows.  The masks go to an LDS ring per wave (mring [wave]
+    // [64 rows][SM] u64, four rows per ds_write), the heavy records to an LDS ring written by
+    // wave 0 (hring [64 rows][kRecWords]).
     // A global store inside the loop would make any later vmcnt(0) wait (a spill reload's, say)
     // wait for that store to reach memory.
     uint64_t pmC[PATHS ? SM : 1] = {};
-    uint32_t* const mring = reinterpret_cast<uint32_t*>(vkeep + 2 * SM * B);  // u64 pairs
+    uint32_t* const mring = reinterpret_cast<uint32_t*>(symr + kChainSymChunk);  // u64 pairs
     uint32_t* const hring = mring + 2 * W * kPathRing * SM;
-    const uint32_t pos0 = t * SM;  // position of slot 0
-    uint32_t pstage = 0;       // light masks of four observations, staged lane by lane
+    uint32_t pstage = 0;  // light masks of four observations, staged lane by lane
+    float* const ckq = PATHS ? b.ckpt + b.ckpt_off[q] : nullptr;
+    auto checkpoint = [&](uint32_t obs, const float (&vv)[SM]) {  // obs % kCkptEvery == 0
+#pragma unroll
+        for (int s = 0; s < SM; ++s) ckq[(size_t)(obs / kCkptEvery) * (SM * B) + s * B + t] = vv[s];
+    };
     if constexpr (PATHS) {
 #pragma unroll
         for (int s = 0; s < SM; ++s) {
             const uint32_t f = m.pflags[s * B + t];
             const bool ec = f & 1u, ea = f & 2u, hl = f & 4u;
             pmC[s] = __builtin_amdgcn_ballot_w64(ea && (!ec || hl));
-            vkeep[s * B + t] = v[s];  // v_0 (the loop keeps v_i at [i & 1])
         }
+        checkpoint(0, v);  // v_0
     }
     // Heavy-row record of observation obs (record row obs-1): the inputs of its backpointers --
     // the heavy scores vo of obs-1 and the light minimum mu of obs-1 -- stored by wave 0; the
     // traceback re-evaluates the lexicographic (value, row) argmin from them with the same float
-    // operations, only where a path passes.  Here only `need` is decided: a valid heavy row whose
-    // new score came from its light-set term (won or tied), so j* must be found.  tgt[h] is that
-    // term, fl(c_A + mu).
-    auto heavy_record = [&](uint32_t obs, float mu, const HeavyConst& hc, const float (&vo)[HM],
-                            float (&tgt)[HM]) -> bool {
-        const float ca[2] = {hc.c0.x, hc.c0.y};  // cst[kBandTailA + h]
-        bool need = false;
-#pragma unroll
-        for (int h = 0; h < HM; ++h) {
-            tgt[h] = ca[h] + mu;
-            need |= m.hvalid[h] && ((m.hl_exist >> h) & 1u) && vh[h] == tgt[h];
-        }
+    // operations, only where a path passes.
+    auto heavy_record = [&](uint32_t obs, float mu, const float (&vo)[HM]) {
         if (wave == 0 && lane == 0) {
             float* r = reinterpret_cast<float*>(hring + ((obs - 1) & (kPathRing - 1)) * kRecWords);
             r[0] = vo[0];
             r[1] = vo[1];
             r[2] = mu;
         }
-        return uniform((int)need) != 0;
     };
-    // j* candidates of this thread: the lowest own light position with fl(c_A + vk[s]) == target,
-    // vk = the kept light scores of the record row's observation.
-    auto jstar_cands = [&](const HeavyConst& hc, const float (&tgt)[HM], uint32_t (&c)[HM], uint32_t parity) {
-        float vk[SM];
-#pragma unroll
-        for (int s = 0; s < SM; ++s) vk[s] = vkeep[parity * (SM * B) + s * B + t];
-        // positions made here (opaque base): hoisted out of the loop they would be spilled
-        uint32_t p0 = pos0;
-        asm volatile("" : "+v"(p0));
-        const float ca[2] = {hc.c0.x, hc.c0.y};  // cst[kBandTailA + h]
-#pragma unroll
-        for (int h = 0; h < HM; ++h) {
-            uint32_t x = ~0u;
-#pragma unroll
-            for (int s = SM - 1; s >= 0; --s) x = (ca[h] + vk[s] == tgt[h]) ? p0 + s : x;
-            c[h] = x;
-        }
-    };
-    static_assert(kBandTailA == 0 && kBandHeavy == 2, "jstar_cands reads cst[kBandTailA + h] from c0.xy");
 
     // Flushes of the staging rings (global layouts: kernels.h, FusedBatch::cmask / hrec).
     auto flush_masks = [&](uint32_t row0) {  // this wave's 32 rows from row0 (a multiple of 32)
@@ -525,7 +438,6 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         for (uint32_t x = lane; x < rows * kRecWords; x += 64)
             dst[x] = hring[((row0 + x / kRecWords) & (kPathRing - 1)) * kRecWords + x % kRecWords];
     };
-    uint32_t jpend[HM] = {~0u, ~0u};     // PATHS: j* candidates waiting for the next publish
     float own_p1 = kInf, own_p2 = kInf;  // W == 1: partials of the last two observations
     uint32_t pc_next = 0;                 // W > 1: count and cell of the observation before the
     float pm_next = kInf;                 // current one, read half a step before they are needed
@@ -611,10 +523,7 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
             StaticFor<0, SM>::run(mask_slot);
         }
         if constexpr (W > 1) {
-            if constexpr (PATHS)  // with the j* candidates found during step i-1
-                publish(slotc, i, row_partial(vn), vn[SM - 1], row_min16_u32(jpend[0]), row_min16_u32(jpend[1]));
-            else
-                publish(slotc, i, row_partial(vn), vn[SM - 1]);
+            publish(slotc, i, row_partial(vn), vn[SM - 1]);
         } else {  // one wave: its own partials are the only ones, keep the last two in registers
             own_p2 = own_p1;
             own_p1 = uniform_f(wave_partial(vn));
@@ -628,35 +537,11 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
                     if ((i & 31u) == 0) flush_masks(i - 32);  // rows i-32 .. i-1 are in the ring
                 }
             }
-            // heavy records of observation i-1 (row i-2) and, when needed, its j* candidates
-            jpend[0] = ~0u;
-            jpend[1] = ~0u;
-            if (lagged) {
-                float tgt[HM];
-                if (heavy_record(i - 1, mu, hc_prev, vo, tgt)) jstar_cands(hc_prev, tgt, jpend, i & 1u);
-                if constexpr (W == 1) {  // one wave: reduce and store now
-#pragma unroll
-                    for (int h = 0; h < HM; ++h) {
-                        const uint32_t r = row_min16_u32(jpend[h]);
-                        const uint32_t a = min((uint32_t)__builtin_amdgcn_readlane((int)r, 15),
-                                               (uint32_t)__builtin_amdgcn_readlane((int)r, 31));
-                        const uint32_t c = min((uint32_t)__builtin_amdgcn_readlane((int)r, 47),
-                                               (uint32_t)__builtin_amdgcn_readlane((int)r, 63));
-                        if (lane == 0) hring[((i - 2) & (kPathRing - 1)) * kRecWords + kRecJ + h] = min(a, c);
-                    }
-                }
-            }
-            if (W > 1 && wave == 0 && i >= 5) {
-                // j* of record row i-5: every row's candidates, published with i-2, arrived with
-                // its count (take_mu above)
-                const uint64_t jw = lds_load64(reinterpret_cast<const uint64_t*>(jcell + 2 * s2));
-                if (lane == 0) *reinterpret_cast<uint64_t*>(hring + ((i - 5) & (kPathRing - 1)) * kRecWords + kRecJ) = jw;
-            }
+            if (lagged) heavy_record(i - 1, mu, vo);  // row i-2
             if constexpr (s0 == 0) {
+                if ((i & (kCkptEvery - 1)) == 0) checkpoint(i, vn);
                 if (wave == 0 && (i & 31u) == 8 && i >= 40) flush_recs(i - 40, 32);  // rows complete
             }
-#pragma unroll
-            for (int s = 0; s < SM; ++s) vkeep[(i & 1u) * (SM * B) + s * B + t] = vn[s];  // after the j* read
         }
 #pragma unroll
         for (int s = 0; s < SM; ++s) v[s] = vn[s];
@@ -753,21 +638,12 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         const uint32_t sl = (len - 2) & (kRing - 1);
         float mu = own_p2;
         if constexpr (W > 1) mu = take_mu(len - 2, sl, pc_next, pm_next);
-        if constexpr (PATHS) {  // record row len-2: its j* straight from the kept scores v_{len-2}
-            float tgt[HM], vo[HM];
-            uint32_t jc[HM] = {~0u, ~0u};
+        if constexpr (PATHS) {  // record row len-2
+            float vo[HM];
 #pragma unroll
             for (int h = 0; h < HM; ++h) vo[h] = vh[h];
-            heavy_update(mu, hc);  // heavy_record's need compares the new heavy scores
-            if (heavy_record(len - 1, mu, hc, vo, tgt)) jstar_cands(hc, tgt, jc, len & 1u);
-#pragma unroll
-            for (int h = 0; h < HM; ++h) {  // jfin[h]: row len-2, jfin[2+h]: row len-3 (pending)
-                const uint32_t r = row_min16_u32(jc[h]), rp = row_min16_u32(jpend[h]);
-                if ((lane & 15u) == 15u) {
-                    __hip_atomic_fetch_min(jfin + h, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_min(jfin + 2 + h, rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
+            heavy_update(mu, hc);
+            heavy_record(len - 1, mu, vo);
         } else {
             heavy_update(mu, hc);
         }
@@ -775,7 +651,6 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     if constexpr (PATHS) {
         if (len > 1 && ((len - 1) & 3u) != 0 && lane < 8 * SM)  // the last, partial block of masks
             mring[(wave * kPathRing + (((len - 2) & ~3u) & (kPathRing - 1))) * (2 * SM) + lane] = pstage;
-        __syncthreads();  // every wave's j* candidates are in
         if (len > 1) {
             // masks not flushed by the loop (it flushed rows below the last multiple of 32 <= len-1)
             const uint32_t mdone = (len - 1) & ~31u;
@@ -787,18 +662,6 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
                 for (uint32_t x = lane; x < cnt; x += 64) dst[x] = src[x];
             }
             if (wave == 0) {
-                if (lane == 0) {
-                    // j* of rows the loop did not finish: len-2 (jfin), and with W > 1 len-3
-                    // (pending candidates), len-4 and len-5 (published with observations len-1, len-2)
-                    auto put = [&](uint32_t row, const uint32_t* c) {
-                        hring[(row & (kPathRing - 1)) * kRecWords + kRecJ] = c[0];
-                        hring[(row & (kPathRing - 1)) * kRecWords + kRecJ + 1] = c[1];
-                    };
-                    put(len - 2, jfin);
-                    if (W > 1 && len >= 3) put(len - 3, jfin + 2);
-                    if (W > 1 && len >= 4) put(len - 4, jcell + 2 * ((len - 1) & (kRing - 1)));
-                    if (W > 1 && len >= 5) put(len - 5, jcell + 2 * ((len - 2) & (kRing - 1)));
-                }
                 // records not flushed by the loop (it flushed rows below i-8 at i = 8 mod 32, i >= 40)
                 const uint32_t hdone = len - 1 >= 40 ? ((len - 1 - 8) & ~31u) : 0u;
                 flush_recs(hdone, len - 1 - hdone);

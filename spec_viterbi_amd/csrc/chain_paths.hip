@@ -30,13 +30,74 @@ const void* chain_paths_fn(int sm, int waves) {
 
 namespace {
 
+constexpr uint32_t kTbMaxCap = 5 * 512;  // SM * B of the largest decoded-path geometry
+
+// j*_h of record row r: the lowest light position p with fl(cA_h + v_r[p]) == fl(cA_h + mu_r),
+// cA_h the light-set constant of heavy row h for the symbol of observation r+1 (the heavy row's
+// light-set argmin, lexicographic (value, row) as the oracle).  v_r is recomputed by the wave
+// from the checkpoint row c = r rounded down to kCkptEvery with the chain kernel's float
+// operations: light v_i[p] = fminf(fl(fl(E + bw) + v_{i-1}[p-1]), fl(fl(E + aw) + vh_{i-1}[0])),
+// heavy vh_i[h] = fminf(fl(cA + mu_{i-1}), fl(cX_h0 + vh_{i-1}[0]), fl(cX_h1 + vh_{i-1}[1])),
+// mu = min of the light scores; vh_c comes from record row c.  buf: 2 * SM * B floats of LDS.
+__device__ uint32_t recompute_jstar(const BandModel& m, const FusedBatch& b, uint32_t q, uint32_t r, uint32_t h,
+                                   float* buf) {
+    const uint32_t lane = threadIdx.x, SM = m.SM, B = m.B, cap = SM * B;
+    const uint32_t* rec = b.hrec + b.hrec_off[q];
+    const uint8_t* sym = b.symbols + b.sym_off[q];
+    const uint32_t c = r / kCkptEvery * kCkptEvery;
+    const float* ck = b.ckpt + b.ckpt_off[q] + (size_t)(c / kCkptEvery) * cap;
+    float* cur = buf;
+    float* nxt = buf + kTbMaxCap;
+    for (uint32_t x = lane; x < cap; x += 64) cur[x] = ck[x];
+    float vh0 = __builtin_bit_cast(float, rec[(size_t)c * kRecWords]);
+    float vh1 = __builtin_bit_cast(float, rec[(size_t)c * kRecWords + 1]);
+    __syncthreads();
+    for (uint32_t i = c + 1; i <= r; ++i) {
+        const float* e = m.erows + (size_t)sym[i] * m.erow;
+        float pm = kInf;
+        for (uint32_t x = lane; x < cap; x += 64) {
+            const uint32_t sl = x / B, t = x % B;
+            const float pv = sl ? cur[x - B] : (t ? cur[(SM - 1) * B + t - 1] : kInf);
+            const float xb = (e[x] + m.bw[x]) + pv;
+            nxt[x] = fminf(xb, (e[x] + m.aw[x]) + vh0);
+            pm = fminf(pm, cur[x]);
+        }
+        for (int off = 32; off >= 1; off >>= 1) pm = fminf(pm, __shfl_xor(pm, off));
+        const float* tl = e + cap;  // heavy constants of sym[i]
+        float n0 = tl[kBandTailA + 0] + pm;
+        n0 = fminf(n0, tl[kBandTailX + 0] + vh0);
+        n0 = fminf(n0, tl[kBandTailX + 1] + vh1);
+        float n1 = tl[kBandTailA + 1] + pm;
+        n1 = fminf(n1, tl[kBandTailX + kBandHeavy] + vh0);
+        n1 = fminf(n1, tl[kBandTailX + kBandHeavy + 1] + vh1);
+        vh0 = n0;
+        vh1 = n1;
+        float* tmp = cur;
+        cur = nxt;
+        nxt = tmp;
+        __syncthreads();
+    }
+    const float mu = __builtin_bit_cast(float, rec[(size_t)r * kRecWords + 2]);
+    const float ca = m.erows[(size_t)sym[r + 1] * m.erow + cap + kBandTailA + h];
+    const float tgt = ca + mu;
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t x = lane; x < cap; x += 64)
+        if (ca + cur[x] == tgt) best = min(best, (x % B) * SM + x / B);  // natural position
+    for (int off = 32; off >= 1; off >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, off));
+    __syncthreads();  // buf is reused by the next call
+    return best;
+}
+
 // Path traceback over the decoded-path variant's records, one wave per sequence.  The walk is
 // speculative along runs: inside a run of chain steps (light position p at observation i came
 // from p-1 at i-1) or of heavy self-loops, lane l reads the record of observation i-l in
 // parallel, and the first lane whose record leaves the run ends the iteration; so a sequence
-// costs about (len / 64 + number of runs) dependent rounds of loads instead of len.
+// costs about (len / 64 + number of runs) dependent rounds of loads instead of len.  A heavy
+// row whose light-set term wins or ties stops the run; if that lane is the first to stop, the
+// wave recomputes its j* (recompute_jstar) and settles it.
 __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedBatch b, const uint64_t* path_off,
                                                               int32_t* paths) {
+    __shared__ float buf[2 * kTbMaxCap];
     const uint32_t q = blockIdx.x, lane = threadIdx.x;
     const uint32_t len = b.end[q];
     const uint32_t SM = m.SM, B = m.B, W = B / 64;
@@ -57,7 +118,10 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
         const int64_t r = i - 1 - (int64_t)lane;  // record row of this lane (observation r+1)
         const bool valid = r >= 0;
         int32_t pred = -1;
-        bool cont = false;
+        bool cont = false, needj = false;
+        float hv = kInf, lv = kInf;
+        uint32_t hcol = 0xFFFFFFFFu;
+        bool hex = false;
         if (pos >= 0) {  // light run: lane l looks at position pos-l at observation i-l
             const int64_t p = (int64_t)pos - (int64_t)lane;
             if (valid && p >= 0) {
@@ -76,17 +140,12 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
         } else if (valid) {  // heavy run: self-loops of heavy row h
             // The heavy row's lexicographic (value, row) argmin at observation r+1, re-evaluated
             // from the recorded inputs with the kernel's float operations (heavy_update): the
-            // heavy-row terms fl(cX + vo[k]) and the light-set term fl(cA + mu), whose lowest row
-            // is the recorded j* (a light position).
+            // heavy-row terms fl(cX + vo[k]) and the light-set term fl(cA + mu).
             const uint32_t h = (uint32_t)(-1 - pos);
             const uint32_t* rw = rec + (uint64_t)r * kRecWords;
             const float vo[2] = {__builtin_bit_cast(float, rw[0]), __builtin_bit_cast(float, rw[1])};
             const float mu = __builtin_bit_cast(float, rw[2]);
-            const uint32_t o = sym[r + 1];
-            const float* tl = m.erows + (size_t)o * m.erow + (size_t)SM * B;  // heavy constants of o
-            float hv = kInf;
-            uint32_t hcol = 0xFFFFFFFFu;
-            bool hex = false;
+            const float* tl = m.erows + (size_t)sym[r + 1] * m.erow + (size_t)SM * B;  // heavy constants
 #pragma unroll
             for (int k = 0; k < kBandHeavy; ++k) {
                 if ((m.hx_exist >> (h * kBandHeavy + k)) & 1u) {
@@ -98,20 +157,28 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
                     hex = true;
                 }
             }
-            uint32_t k = hex ? hcol : 0xFFFFFFFFu;
+            pred = hex ? (int32_t)hcol : -1;
             if ((m.hl_exist >> h) & 1u) {
-                const float lv = tl[kBandTailA + h] + mu;
-                if (!hex || !(hv < lv)) {  // the light set wins or ties: its lowest row j*
-                    const uint32_t jp = rw[kRecJ + h];
-                    const uint32_t js = m.lrow[(jp % SM) * B + jp / SM];
-                    k = !hex || lv < hv ? js : min(hcol, js);
-                }
+                lv = tl[kBandTailA + h] + mu;
+                needj = !hex || !(hv < lv);  // the light set wins or ties: its lowest row j* decides
             }
-            pred = k == 0xFFFFFFFFu ? -1 : (int32_t)k;
-            cont = pred == s;
+            cont = !needj && pred == s;
         }
-        const uint64_t stop = __builtin_amdgcn_ballot_w64(!cont);
-        const uint32_t ls = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;  // first lane leaving the run
+        uint64_t stop = __builtin_amdgcn_ballot_w64(!cont);
+        uint32_t ls = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;  // first lane leaving the run
+        while (ls < 64u && __builtin_amdgcn_readlane((int)needj, (int)ls)) {
+            const uint32_t rs = (uint32_t)(i - 1 - (int64_t)ls);
+            const uint32_t jp = recompute_jstar(m, b, q, rs, (uint32_t)(-1 - pos), buf);
+            if (lane == ls) {
+                const uint32_t js = m.lrow[(jp % SM) * B + jp / SM];
+                const uint32_t k = !hex || lv < hv ? js : min(hcol, js);
+                pred = k == 0xFFFFFFFFu ? -1 : (int32_t)k;
+                cont = pred == s;
+                needj = false;
+            }
+            stop = __builtin_amdgcn_ballot_w64(!cont);
+            ls = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
+        }
         // entries written this round: the run's lanes plus the leaving lane if it has a record
         const uint32_t k = ls == 64u ? 64u : ((int64_t)ls <= i - 1 ? ls + 1u : ls);
         if (lane < k) out[r] = pred;
@@ -129,7 +196,8 @@ bool chain_paths_supported(int sm, int waves) { return chain_paths_fn(sm, waves)
 
 hipError_t launch_chain_traceback(const BandModel& m, const FusedBatch& b, const uint64_t* path_off,
                                   int32_t* paths, hipStream_t stream) {
-    if (!b.cmask || !b.hrec || m.B % 64 || !m.spos || !m.pflags) return hipErrorInvalidValue;
+    if (!b.cmask || !b.hrec || !b.ckpt || m.B % 64 || m.SM * m.B > kTbMaxCap || !m.spos || !m.pflags)
+        return hipErrorInvalidValue;
     if (b.nseq == 0) return hipSuccess;
     hipLaunchKernelGGL(chain_traceback_kernel, dim3(b.nseq), dim3(64), 0, stream, m, b, path_off, paths);
     return hipGetLastError();
@@ -141,7 +209,7 @@ hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStre
     const int sm = (int)m.SM;
     const void* fn = ha == 1 ? chain_fn_ha1(sm, waves, ge) : ha == 2 ? chain_fn_ha2(sm, waves, ge) : nullptr;
     if (b.cmask) {  // decoded paths
-        if (ge || ha != 1 || !b.hrec || !m.pflags) return hipErrorInvalidValue;
+        if (ge || ha != 1 || !b.hrec || !b.ckpt || !m.pflags) return hipErrorInvalidValue;
         fn = chain_paths_fn(sm, waves);
     } else if (ha == 1 && (m.dbg & (4u | 64u | 2048u | 4096u))) {
         if (const void* d = chain_diag_fn(sm, waves, ge, m.dbg)) fn = d;
@@ -153,7 +221,7 @@ hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStre
     BandModel mm = m;
     FusedBatch bb = b;
     void* args[] = {&mm, &bb};
-    // decoded paths keep the light scores of two observations in LDS
+    // decoded paths stage their masks and heavy records in LDS
     const size_t lds = chain_lds_bytes() + (b.cmask ? chain_path_lds_bytes(m.B / 64, m.SM) : 0);
     return hipLaunchKernel(fn, dim3(b.nseq), dim3(m.B), args, lds, stream);
 }

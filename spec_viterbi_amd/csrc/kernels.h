@@ -60,13 +60,17 @@ struct FusedBatch {
     //   cmask: one 64-bit lane mask per (wave, slot): bit = "light position took its heavy term";
     //          layout [r/32][wave][r%32][slot] u64, blocks of 32 rows
     //   hrec:  [r][kRecWords] u32: [0..1] the heavy scores of observation r (f32), [2] the light
-    //          minimum of observation r (f32), [kRecJ + h] = j*: the lowest light position whose
-    //          term achieves heavy row h's light-set minimum (written when that term won or tied);
-    //          the traceback re-evaluates the heavy rows' argmin from these (chain_paths.hip)
+    //          minimum of observation r (f32); the traceback re-evaluates the heavy rows' argmin
+    //          from these (chain_paths.hip)
+    //   ckpt:  the light scores of every kCkptEvery-th observation ([c / kCkptEvery][SM * B],
+    //          slot-major like the model tables): the traceback recomputes a row's light scores
+    //          from the checkpoint below it where it needs the light-set argmin j*
     uint64_t* cmask;
     const uint64_t* cmask_off;  // [nseq] u64 offset of sequence q's masks
     uint32_t* hrec;
     const uint64_t* hrec_off;   // [nseq] u32 offset of sequence q's records
+    float* ckpt;
+    const uint64_t* ckpt_off;   // [nseq] float offset of sequence q's checkpoint rows
     uint32_t nseq;
 };
 
@@ -121,12 +125,11 @@ constexpr int kChainMaxSym = 32;
 constexpr int kChainMaxThreads = 512;
 constexpr uint32_t kChainSymChunk = 32768;  // symbols staged in LDS per refill
 constexpr int kChainRing = 8;  // exchange ring depth (observations in flight between waves)
-inline size_t chain_lds_bytes(size_t kept_floats = 0) {
+inline size_t chain_lds_bytes() {
     // heavy constants | tagged records [ring][waves][2] u64 | cells, counts, junk [ring] 4 B each |
-    // reduction | path cells: j* [ring][2], final [2] + pad, junk [16] (u32) | staged symbols
+    // reduction | staged symbols
     return (size_t)kChainMaxSym * kBandTail * sizeof(float) + (size_t)kChainRing * 2 * kMaxWaves * 8 +
-           3 * kChainRing * 4 + 2 * kMaxWaves * sizeof(float) + (2 * kChainRing + 4 + 16) * 4 +
-           kChainSymChunk + kept_floats * sizeof(float);
+           3 * kChainRing * 4 + 2 * kMaxWaves * sizeof(float) + kChainSymChunk;
 }
 // Chain kernel for (SM slots, W waves, HA heavy feeders, E streamed?); false if not instantiated.
 bool chain_supported(int sm, int waves, int ha, bool ge);
@@ -141,14 +144,19 @@ hipError_t launch_chain_traceback(const BandModel& m, const FusedBatch& b, const
 inline uint64_t chain_mask_words(uint64_t len, uint32_t waves, uint32_t sm) {
     return len > 1 ? (len - 1 + 31) / 32 * 32 * (uint64_t)waves * sm : 0;
 }
-// Decoded-path staging in LDS: ring depth (rows) and bytes beyond chain_lds_bytes(): the kept
-// scores of two observations, the mask ring and the heavy-record ring.
+// Decoded-path staging in LDS: ring depth (rows) and bytes beyond chain_lds_bytes(): the mask
+// ring and the heavy-record ring.
 constexpr uint32_t kPathRing = 64;
+constexpr uint32_t kRecWords = 4;
 inline size_t chain_path_lds_bytes(uint32_t waves, uint32_t sm) {
-    return (size_t)2 * sm * 64 * waves * 4 + (size_t)waves * kPathRing * sm * 8 + (size_t)kPathRing * 8 * 4;
+    return (size_t)waves * kPathRing * sm * 8 + (size_t)kPathRing * kRecWords * 4;
 }
-constexpr uint32_t kRecWords = 8, kRecJ = 4;
 inline uint64_t chain_hrec_words(uint64_t len) { return len > 1 ? (len - 1) * kRecWords : 0; }
+// Light-score checkpoints of the decoded-path variant: rows 0, kCkptEvery, ... <= len-1.
+constexpr uint32_t kCkptEvery = 16;
+inline uint64_t chain_ckpt_floats(uint64_t len, uint32_t sm, uint32_t threads) {
+    return len ? ((len - 1) / kCkptEvery + 1) * (uint64_t)sm * threads : 0;
+}
 
 // CSR of T^T used by the generic kernel and the _spec precompute.
 struct CsrModel {

@@ -835,7 +835,8 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
     h_bpoff.resize(nseq);
     h_cmoff.resize(nseq);
     h_hroff.resize(nseq);
-    uint64_t bytes = 0, bpn = 0, cmn = 0, hrn = 0;
+    h_ckoff.resize(nseq);
+    uint64_t bytes = 0, bpn = 0, cmn = 0, hrn = 0, ckn = 0;
     for (uint32_t q = 0; q < nseq; ++q) {
         if (offs[q + 1] < offs[q]) throw Error(SVH_E_INVALID, "offsets must be non-decreasing");
         const uint64_t len = offs[q + 1] - offs[q];
@@ -850,6 +851,8 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
             cmn += chain_mask_words(len, cpl->plan.B / 64, cpl->plan.SM);
             h_hroff[q] = hrn;
             hrn += chain_hrec_words(len);
+            h_ckoff[q] = ckn;
+            ckn += chain_ckpt_floats(len, cpl->plan.SM, cpl->plan.B);
         } else if (paths) {
             h_bpoff[q] = bpn;
             bpn += (len - 1) * (uint64_t)model->host.n;
@@ -882,6 +885,8 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
         d_cmaskoff.upload_async(h_cmoff.data(), (size_t)nseq * 8, s);
         d_hrec.reserve((size_t)std::max<uint64_t>(hrn, kRecWords) * 4);
         d_hrecoff.upload_async(h_hroff.data(), (size_t)nseq * 8, s);
+        d_ckpt.reserve((size_t)std::max<uint64_t>(ckn, 1) * 4);
+        d_ckptoff.upload_async(h_ckoff.data(), (size_t)nseq * 8, s);
     } else if (paths) {
         d_bp.reserve((size_t)std::max<uint64_t>(bpn, 1) * 2);
         d_bpoff.upload_async(h_bpoff.data(), (size_t)nseq * 8, s);
@@ -924,6 +929,8 @@ void Batch::run(uint32_t level, hipStream_t s) {
         fb.cmask_off = d_cmaskoff.as<uint64_t>();
         fb.hrec = d_hrec.as<uint32_t>();
         fb.hrec_off = d_hrecoff.as<uint64_t>();
+        fb.ckpt = d_ckpt.as<float>();
+        fb.ckpt_off = d_ckptoff.as<uint64_t>();
     } else if (paths) {
         fb.bp = d_bp.as<uint16_t>();
         fb.bp_off = d_bpoff.as<uint64_t>();

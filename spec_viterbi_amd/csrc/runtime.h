@@ -162,7 +162,7 @@ struct Batch {
     DeviceBuffer d_sym, d_symoff, d_begin, d_end, d_scores, d_best;
     DeviceBuffer d_bp, d_bpoff, d_pathoff, d_paths;
     bool chain_paths = false;  // paths from the chain kernel's compact records (else fused / generic)
-    DeviceBuffer d_cmask, d_cmaskoff, d_hrec, d_hrecoff;
+    DeviceBuffer d_cmask, d_cmaskoff, d_hrec, d_hrecoff, d_ckpt, d_ckptoff;
     // _spec runs
     DeviceBuffer d_vbuf, d_nchunks, d_tbegin, d_vrow;
     uint32_t spec_ready_level = 0;
@@ -172,7 +172,7 @@ struct Batch {
 
     // host staging of the last load (kept alive for the asynchronous uploads)
     std::vector<uint8_t> h_sym;
-    std::vector<uint64_t> h_symoff, h_pathoff, h_bpoff, h_cmoff, h_hroff;
+    std::vector<uint64_t> h_symoff, h_pathoff, h_bpoff, h_cmoff, h_hroff, h_ckoff;
     std::vector<uint32_t> h_zero;
 
     Batch(Model* m, uint64_t nseq, const uint64_t* offsets, const uint64_t* symbols, uint32_t flags);

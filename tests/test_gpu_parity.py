@@ -242,8 +242,9 @@ def test_chain_random_models(L, kw, seed):
     (300, {"feed_c": True}, 8),                       # two heavy feeders: fused paths
 ])
 def test_chain_decoded_paths(L, kw, seed):
-    """Decoded paths from the chain kernel's compact records (light lane masks, heavy-row records
-    with the j* second pass) and the speculative traceback: scores, best states and every path
+    """Decoded paths from the chain kernel's compact records (light lane masks, heavy-row records,
+    score checkpoints that the traceback recomputes j* from) and the speculative traceback: scores,
+    best states and every path
     entry identical to the oracle's lexicographic (value, row) argmin, over lengths 1..5000."""
     hmm = random_chain_hmm(L, seed=seed, **kw)
     seqs = random_seqs(20, [1, 2, 3, 4, 5, 6, 7, 8, 9, 63, 64, 65, 77, 1000, 5000], seed=seed)
