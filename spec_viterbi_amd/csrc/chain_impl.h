@@ -115,19 +115,25 @@ __device__ __forceinline__ float row_min16(float x) {
     return x;
 }
 
-// dst[L] = x (x wave-uniform, in an SGPR; the lane an inline constant: one constant-bus read).
-// x must be written by an SALU instruction (mask_code below): read straight after the VALU
-// compare that wrote it, v_writelane took a stale value on MI355X (wrong lane masks), and hipcc
-// pads no hazard for an asm consumer.
-template <uint32_t L>
-__device__ __forceinline__ void writelane(uint32_t& dst, uint32_t x) {
-    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(x), "n"(L));
+// acc = (acc << 1) | bit per lane: v_addc acc + acc + carry, the carry-in the 64-bit lane mask.
+// The mask reaches the VALU through an SALU instruction: read straight after the VALU compare
+// that wrote it, an SGPR operand came back stale on MI355X (hipcc pads no hazard for an asm
+// consumer).  push_bit: bit = lt | (eq & c); push_bit1: bit = m.
+__device__ __forceinline__ void push_bit(uint32_t& acc, uint64_t lt, uint64_t eq, uint64_t c) {
+    uint64_t k, co;
+    asm volatile("s_and_b64 %1, %4, %5\n\t"
+                 "s_or_b64 %1, %1, %3\n\t"
+                 "v_addc_co_u32_e64 %0, %2, %0, %0, %1"
+                 : "+v"(acc), "=&s"(k), "=&s"(co)
+                 : "s"(lt), "s"(eq), "s"(c)
+                 : "scc");
 }
-// lt | (c & eq) on SALU (see writelane)
-__device__ __forceinline__ uint64_t mask_code(uint64_t lt, uint64_t eq, uint64_t c) {
-    uint64_t r;
-    asm volatile("s_and_b64 %0, %2, %3\n\ts_or_b64 %0, %0, %1" : "=&s"(r) : "s"(lt), "s"(eq), "s"(c) : "scc");
-    return r;
+__device__ __forceinline__ void push_bit1(uint32_t& acc, uint64_t m) {
+    uint64_t k, co;
+    asm volatile("s_mov_b64 %1, %3\n\t"
+                 "v_addc_co_u32_e64 %0, %2, %0, %0, %1"
+                 : "+v"(acc), "=&s"(k), "=&s"(co)
+                 : "s"(m));
 }
 
 // f(integral_constant<int, I>) for I in [I0, N): a loop whose index is a constant expression
@@ -157,15 +163,16 @@ __device__ __forceinline__ unsigned long long stamp() {
 // observation, in the order of the oracle's lexicographic (value, row) argmin.  All of it runs
 // after the observation's publish, off the inter-wave critical path:
 //   * light position p: its two candidates (position p-1, heavy row 0) are compared in every lane
-//     and one 64-bit lane mask per slot records "took the heavy term" (staged in a VGPR by
-//     v_writelane, stored every four observations);
+//     and one bit per lane and slot records "took the heavy term", shifted into a register that
+//     holds the last 32 observations and is stored every 32 (PATHS 2: every heavy term wins
+//     ties, one compare per slot);
 //   * heavy row h: its argmin is re-evaluated by the traceback from the heavy scores and the
 //     light minimum of the observation before (wave 0 records them).  Where the light-set term
 //     wins or ties, the traceback also needs j* = the lowest light position with
 //     fl(c + v[j]) == fl(c + min v): it recomputes that row's light scores from a checkpoint
 //     (every kCkptEvery-th row of light scores, stored here) instead of this kernel finding j*
 //     for every observation (on 2405.chmm the path needs it about once per sequence).
-template <int SM, int W, int HA, bool GE, bool STAMP = false, int DIAG = 0, bool PATHS = false>
+template <int SM, int W, int HA, bool GE, bool STAMP = false, int DIAG = 0, int PATHS = 0>
 __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
     static_assert(!PATHS || (HA == 1 && !GE && !STAMP && DIAG == 0), "decoded paths: HA 1, E in VGPRs");
     constexpr int HM = kBandHeavy;
@@ -388,16 +395,17 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
     // [xh == xb]): without a heavy term xh = +inf is never below xb and C drops the tie; without
     // a chain term xb = +inf, so the heavy term is taken.
     //
-    // Output staging: nothing is stored to HBM inside the loop except one flush per 32
-    // observations and the checkpoint rows.  The masks go to an LDS ring per wave (mring [wave]
-    // [64 rows][SM] u64, four rows per ds_write), the heavy records to an LDS ring written by
-    // wave 0 (hring [64 rows][kRecWords]).
-    // A global store inside the loop would make any later vmcnt(0) wait (a spill reload's, say)
-    // wait for that store to reach memory.
+    // Output: the mask words (one per lane and slot) every 32 observations, the checkpoint rows
+    // every kCkptEvery, and the heavy records, staged in an LDS ring written by wave 0 (hring
+    // [64 rows][kRecWords]) and flushed every 32 observations.
     uint64_t pmC[PATHS ? SM : 1] = {};
-    uint32_t* const mring = reinterpret_cast<uint32_t*>(symr + kChainSymChunk);  // u64 pairs
-    uint32_t* const hring = mring + 2 * W * kPathRing * SM;
-    uint32_t pstage = 0;  // light masks of four observations, staged lane by lane
+    uint32_t macc[PATHS ? SM : 1] = {};  // bit k: record row (last row) - k
+    uint32_t* const hring = reinterpret_cast<uint32_t*>(symr + kChainSymChunk);
+    uint32_t* const cmq = PATHS ? b.cmask + b.cmask_off[q] : nullptr;
+    auto store_masks = [&](uint32_t row0, uint32_t rows) {  // rows row0 .. row0+rows-1, row0 % 32 == 0
+#pragma unroll
+        for (int s = 0; s < SM; ++s) cmq[((size_t)(row0 >> 5) * SM + s) * B + t] = macc[s] << (32u - rows);
+    };
     float* const ckq = PATHS ? b.ckpt + b.ckpt_off[q] : nullptr;
     auto checkpoint = [&](uint32_t obs, const float (&vv)[SM]) {  // obs % kCkptEvery == 0
 #pragma unroll
@@ -425,14 +433,7 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         }
     };
 
-    // Flushes of the staging rings (global layouts: kernels.h, FusedBatch::cmask / hrec).
-    auto flush_masks = [&](uint32_t row0) {  // this wave's 32 rows from row0 (a multiple of 32)
-        const uint32_t* src = mring + (wave * kPathRing + (row0 & (kPathRing - 1))) * (2 * SM);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(b.cmask + b.cmask_off[q]) +
-                        ((size_t)(row0 >> 5) * W + wave) * (32 * 2 * SM);
-#pragma unroll
-        for (int k = 0; k < SM; ++k) dst[k * 64 + lane] = src[k * 64 + lane];
-    };
+    // Flush of the record ring (global layout: kernels.h, FusedBatch::hrec).
     auto flush_recs = [&](uint32_t row0, uint32_t rows) {  // wave 0: rows row0 .. row0+rows-1
         uint32_t* dst = b.hrec + b.hrec_off[q] + (size_t)row0 * kRecWords;
         for (uint32_t x = lane; x < rows * kRecWords; x += 64)
@@ -507,18 +508,18 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
             for (int h = 0; h < HA; ++h) r = fminf(r, xa[h][0] + vh[h]);
             vn[0] = lane == 0 ? r : vn[0];
         }
-        if constexpr (PATHS) {  // light masks of observation i (record row i-1), staged lane by lane
-            constexpr uint32_t L0 = ((s0 + kRing - 1) & 3u) * (2 * SM);
+        if constexpr (PATHS) {  // light masks of observation i (record row i-1)
             auto mask_slot = [&](auto sc) {
                 constexpr int s = decltype(sc)::value;
                 const float xh = xa[0][s] + vh[0];
                 const float xbe = s == 0 ? xb0 : xb[s];
                 // heavy term taken: below the chain term, or tied and winning the tie
-                const uint64_t lt = __builtin_amdgcn_ballot_w64(xh < xbe);
-                const uint64_t eq = __builtin_amdgcn_ballot_w64(xh == xbe);
-                const uint64_t code = mask_code(lt, eq, pmC[s]);
-                writelane<L0 + 2 * s>(pstage, (uint32_t)code);
-                writelane<L0 + 2 * s + 1>(pstage, (uint32_t)(code >> 32));
+                if constexpr (PATHS == 2) {
+                    push_bit1(macc[s], __builtin_amdgcn_ballot_w64(xh <= xbe));
+                } else {
+                    push_bit(macc[s], __builtin_amdgcn_ballot_w64(xh < xbe), __builtin_amdgcn_ballot_w64(xh == xbe),
+                             pmC[s]);
+                }
             };
             StaticFor<0, SM>::run(mask_slot);
         }
@@ -530,15 +531,9 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         }
         mark(4);
         if constexpr (PATHS) {
-            // light masks of observation i (record row i-1) were staged before the publish
-            if constexpr ((s0 & 3u) == 0) {  // rows i-4 .. i-1 staged: one store per wave
-                if (lane < 8 * SM) mring[(wave * kPathRing + ((i - 4) & (kPathRing - 1))) * (2 * SM) + lane] = pstage;
-                if constexpr (s0 == 0) {
-                    if ((i & 31u) == 0) flush_masks(i - 32);  // rows i-32 .. i-1 are in the ring
-                }
-            }
             if (lagged) heavy_record(i - 1, mu, vo);  // row i-2
             if constexpr (s0 == 0) {
+                if ((i & 31u) == 0) store_masks(i - 32, 32);  // rows i-32 .. i-1 are in macc
                 if ((i & (kCkptEvery - 1)) == 0) checkpoint(i, vn);
                 if (wave == 0 && (i & 31u) == 8 && i >= 40) flush_recs(i - 40, 32);  // rows complete
             }
@@ -649,18 +644,10 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
         }
     }
     if constexpr (PATHS) {
-        if (len > 1 && ((len - 1) & 3u) != 0 && lane < 8 * SM)  // the last, partial block of masks
-            mring[(wave * kPathRing + (((len - 2) & ~3u) & (kPathRing - 1))) * (2 * SM) + lane] = pstage;
         if (len > 1) {
-            // masks not flushed by the loop (it flushed rows below the last multiple of 32 <= len-1)
+            // masks not stored by the loop (it stored rows below the last multiple of 32 <= len-1)
             const uint32_t mdone = (len - 1) & ~31u;
-            if (mdone < len - 1) {
-                const uint32_t* src = mring + (wave * kPathRing + (mdone & (kPathRing - 1))) * (2 * SM);
-                uint32_t* dst = reinterpret_cast<uint32_t*>(b.cmask + b.cmask_off[q]) +
-                                ((size_t)(mdone >> 5) * W + wave) * (32 * 2 * SM);
-                const uint32_t cnt = (len - 1 - mdone) * 2 * SM;
-                for (uint32_t x = lane; x < cnt; x += 64) dst[x] = src[x];
-            }
+            if (mdone < len - 1) store_masks(mdone, len - 1 - mdone);
             if (wave == 0) {
                 // records not flushed by the loop (it flushed rows below i-8 at i = 8 mod 32, i >= 40)
                 const uint32_t hdone = len - 1 >= 40 ? ((len - 1 - 8) & ~31u) : 0u;
@@ -739,6 +726,6 @@ const void* chain_ptr_w(int sm, bool ge) {
 const void* chain_fn_ha1(int sm, int waves, bool ge);    // chain_ha1.hip
 const void* chain_fn_ha2(int sm, int waves, bool ge);    // chain_ha2.hip
 const void* chain_diag_fn(int sm, int waves, bool ge, uint32_t dbg);  // chain_ha1.hip: stamps, ablations
-const void* chain_paths_fn(int sm, int waves);           // chain_paths.hip
+const void* chain_paths_fn(int sm, int waves, bool ties_heavy);  // chain_paths.hip
 
 }  // namespace svh

@@ -4,27 +4,32 @@
 namespace svh {
 namespace {
 
-// Decoded-path variant: E in VGPRs, HA 1 (a model with no heavy feeder runs it too).
-template <int W>
+// Decoded-path variant: E in VGPRs, HA 1 (a model with no heavy feeder runs it too); P = 2 when
+// every heavy term wins its ties (one compare per mask bit), 1 otherwise.
+template <int W, int P>
 const void* chain_paths_ptr_w(int sm) {
     switch (sm) {
 #define SVH_CASE(SMV) \
-    case SMV: return reinterpret_cast<const void*>(&chain_viterbi_kernel<SMV, W, 1, false, false, 0, true>);
+    case SMV: return reinterpret_cast<const void*>(&chain_viterbi_kernel<SMV, W, 1, false, false, 0, P>);
         SVH_CASE(1) SVH_CASE(2) SVH_CASE(3) SVH_CASE(4) SVH_CASE(5)
 #undef SVH_CASE
         default: return nullptr;
     }
 }
-}  // namespace
-
-const void* chain_paths_fn(int sm, int waves) {
+template <int P>
+const void* chain_paths_ptr(int sm, int waves) {
     switch (waves) {
-        case 1: return chain_paths_ptr_w<1>(sm);
-        case 2: return chain_paths_ptr_w<2>(sm);
-        case 4: return chain_paths_ptr_w<4>(sm);
-        case 8: return chain_paths_ptr_w<8>(sm);
+        case 1: return chain_paths_ptr_w<1, P>(sm);
+        case 2: return chain_paths_ptr_w<2, P>(sm);
+        case 4: return chain_paths_ptr_w<4, P>(sm);
+        case 8: return chain_paths_ptr_w<8, P>(sm);
         default: return nullptr;
     }
+}
+}  // namespace
+
+const void* chain_paths_fn(int sm, int waves, bool ties_heavy) {
+    return ties_heavy ? chain_paths_ptr<2>(sm, waves) : chain_paths_ptr<1>(sm, waves);
 }
 
 
@@ -100,8 +105,8 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
     __shared__ float buf[2 * kTbMaxCap];
     const uint32_t q = blockIdx.x, lane = threadIdx.x;
     const uint32_t len = b.end[q];
-    const uint32_t SM = m.SM, B = m.B, W = B / 64;
-    const uint64_t* msk = b.cmask + b.cmask_off[q];
+    const uint32_t SM = m.SM, B = m.B;
+    const uint32_t* msk = b.cmask + b.cmask_off[q];
     const uint32_t* rec = b.hrec + b.hrec_off[q];
     int32_t* out = paths + path_off[q];
     const uint8_t* sym = b.symbols + b.sym_off[q];
@@ -126,10 +131,9 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
             const int64_t p = (int64_t)pos - (int64_t)lane;
             if (valid && p >= 0) {
                 const uint32_t tt = (uint32_t)p / SM, ss = (uint32_t)p % SM;
-                const uint64_t word =
-                    msk[((((uint64_t)r >> 5) * W + tt / 64) * 32 + ((uint32_t)r & 31u)) * SM + ss];
+                const uint32_t word = msk[(((uint64_t)r >> 5) * SM + ss) * B + tt];
                 const uint32_t f = m.pflags[ss * B + tt];
-                if ((word >> (tt & 63u)) & 1ull) {
+                if ((word >> (31u - ((uint32_t)r & 31u))) & 1u) {
                     pred = m.hrow[0];
                 } else if ((f & 1u) && p >= 1) {
                     const uint32_t pp = (uint32_t)p - 1;
@@ -192,7 +196,7 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
 bool chain_supported(int sm, int waves, int ha, bool ge) {
     return (ha == 1 ? chain_fn_ha1(sm, waves, ge) : ha == 2 ? chain_fn_ha2(sm, waves, ge) : nullptr) != nullptr;
 }
-bool chain_paths_supported(int sm, int waves) { return chain_paths_fn(sm, waves) != nullptr; }
+bool chain_paths_supported(int sm, int waves) { return chain_paths_fn(sm, waves, false) != nullptr; }
 
 hipError_t launch_chain_traceback(const BandModel& m, const FusedBatch& b, const uint64_t* path_off,
                                   int32_t* paths, hipStream_t stream) {
@@ -210,7 +214,7 @@ hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStre
     const void* fn = ha == 1 ? chain_fn_ha1(sm, waves, ge) : ha == 2 ? chain_fn_ha2(sm, waves, ge) : nullptr;
     if (b.cmask) {  // decoded paths
         if (ge || ha != 1 || !b.hrec || !b.ckpt || !m.pflags) return hipErrorInvalidValue;
-        fn = chain_paths_fn(sm, waves);
+        fn = chain_paths_fn(sm, waves, m.ties_heavy != 0);
     } else if (ha == 1 && (m.dbg & (4u | 64u | 2048u | 4096u))) {
         if (const void* d = chain_diag_fn(sm, waves, ge, m.dbg)) fn = d;
     }
@@ -222,7 +226,7 @@ hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStre
     FusedBatch bb = b;
     void* args[] = {&mm, &bb};
     // decoded paths stage their masks and heavy records in LDS
-    const size_t lds = chain_lds_bytes() + (b.cmask ? chain_path_lds_bytes(m.B / 64, m.SM) : 0);
+    const size_t lds = chain_lds_bytes() + (b.cmask ? chain_path_lds_bytes() : 0);
     return hipLaunchKernel(fn, dim3(b.nseq), dim3(m.B), args, lds, stream);
 }
 

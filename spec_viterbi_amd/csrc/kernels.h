@@ -57,16 +57,16 @@ struct FusedBatch {
     uint16_t* bp;              // backpointers (PATHS only)
     const uint64_t* bp_off;    // [nseq] element offset of sequence q's (len-1) x n block
     // Chain-kernel decoded paths (chain.hip): per backpointer row r (observation r+1)
-    //   cmask: one 64-bit lane mask per (wave, slot): bit = "light position took its heavy term";
-    //          layout [r/32][wave][r%32][slot] u64, blocks of 32 rows
+    //   cmask: bit = "light position took its heavy term"; u32 words [r/32][slot][thread], bit
+    //          31 - r%32 of a word is row r (position thread*SM + slot)
     //   hrec:  [r][kRecWords] u32: [0..1] the heavy scores of observation r (f32), [2] the light
     //          minimum of observation r (f32); the traceback re-evaluates the heavy rows' argmin
     //          from these (chain_paths.hip)
     //   ckpt:  the light scores of every kCkptEvery-th observation ([c / kCkptEvery][SM * B],
     //          slot-major like the model tables): the traceback recomputes a row's light scores
     //          from the checkpoint below it where it needs the light-set argmin j*
-    uint64_t* cmask;
-    const uint64_t* cmask_off;  // [nseq] u64 offset of sequence q's masks
+    uint32_t* cmask;
+    const uint64_t* cmask_off;  // [nseq] u32 offset of sequence q's masks
     uint32_t* hrec;
     const uint64_t* hrec_off;   // [nseq] u32 offset of sequence q's records
     float* ckpt;
@@ -116,6 +116,8 @@ struct BandModel {
     const int32_t* spos;    // [n] position of a light row, -1-h for heavy row h
     uint32_t hx_exist;      // bit h*kBandHeavy+k: heavy row k -> heavy row h term exists
     uint32_t hl_exist;      // bit h: heavy row h has the shared term from every light row
+    uint32_t ties_heavy;    // 1: every light position with a heavy term has it win ties (one
+                            // compare per mask bit)
 };
 constexpr int kBandStamps = 8;
 
@@ -140,17 +142,14 @@ hipError_t launch_chain(const BandModel& m, int ha, const FusedBatch& b, hipStre
 // Path traceback over the chain kernel's compact backpointers (one wave per sequence).
 hipError_t launch_chain_traceback(const BandModel& m, const FusedBatch& b, const uint64_t* path_off,
                                   int32_t* paths, hipStream_t stream);
-// u64 masks / u32 records the decoded-path variant writes for a sequence of length len.
+// u32 mask words / u32 records the decoded-path variant writes for a sequence of length len.
 inline uint64_t chain_mask_words(uint64_t len, uint32_t waves, uint32_t sm) {
-    return len > 1 ? (len - 1 + 31) / 32 * 32 * (uint64_t)waves * sm : 0;
+    return len > 1 ? (len - 1 + 31) / 32 * (uint64_t)sm * 64 * waves : 0;
 }
-// Decoded-path staging in LDS: ring depth (rows) and bytes beyond chain_lds_bytes(): the mask
-// ring and the heavy-record ring.
+// Decoded-path staging in LDS beyond chain_lds_bytes(): the heavy-record ring (rows).
 constexpr uint32_t kPathRing = 64;
 constexpr uint32_t kRecWords = 4;
-inline size_t chain_path_lds_bytes(uint32_t waves, uint32_t sm) {
-    return (size_t)waves * kPathRing * sm * 8 + (size_t)kPathRing * kRecWords * 4;
-}
+inline size_t chain_path_lds_bytes() { return (size_t)kPathRing * kRecWords * 4; }
 inline uint64_t chain_hrec_words(uint64_t len) { return len > 1 ? (len - 1) * kRecWords : 0; }
 // Light-score checkpoints of the decoded-path variant: rows 0, kCkptEvery, ... <= len-1.
 constexpr uint32_t kCkptEvery = 16;

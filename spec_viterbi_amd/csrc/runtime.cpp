@@ -497,6 +497,7 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
         if (HA >= 1 && aex[order[0]][p]) f |= 2;
         if (HA >= 1 && p > 0 && heavy[order[0]] < light[p - 1]) f |= 4;
         bp.pflags[x] = f;
+        bp.ties_heavy = (p == 0 ? true : bp.ties_heavy) && (f & 2) && (!(f & 1) || (f & 4));
         bp.spos[light[p]] = (int32_t)p;
     }
     for (size_t x = 0; x < order.size(); ++x) bp.spos[heavy[order[x]]] = -1 - (int32_t)x;
@@ -549,6 +550,7 @@ void DeviceBandPlan::upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream
     view.spos = d_spos.as<int32_t>();
     view.hx_exist = p.hx_exist;
     view.hl_exist = p.hl_exist;
+    view.ties_heavy = p.ties_heavy ? 1u : 0u;
     for (int h = 0; h < kBandHeavy; ++h) {
         view.hrow[h] = p.hrow[h];
         view.hvalid[h] = p.hvalid[h];
@@ -881,7 +883,7 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
     d_scores.reserve((size_t)nseq * model->host.n * 4);
     d_best.reserve((size_t)nseq * 8);
     if (paths && chain_paths) {
-        d_cmask.reserve((size_t)std::max<uint64_t>(cmn, 1) * 8);
+        d_cmask.reserve((size_t)std::max<uint64_t>(cmn, 1) * 4);
         d_cmaskoff.upload_async(h_cmoff.data(), (size_t)nseq * 8, s);
         d_hrec.reserve((size_t)std::max<uint64_t>(hrn, kRecWords) * 4);
         d_hrecoff.upload_async(h_hroff.data(), (size_t)nseq * 8, s);
@@ -925,7 +927,7 @@ void Batch::run(uint32_t level, hipStream_t s) {
     fb.best = d_best.as<int64_t>();
     fb.nseq = nseq;
     if (paths && chain_paths) {
-        fb.cmask = d_cmask.as<uint64_t>();
+        fb.cmask = d_cmask.as<uint32_t>();
         fb.cmask_off = d_cmaskoff.as<uint64_t>();
         fb.hrec = d_hrec.as<uint32_t>();
         fb.hrec_off = d_hrecoff.as<uint64_t>();

@@ -107,6 +107,7 @@ struct BandPlan {
     std::vector<uint8_t> pflags;  // decoded paths (BandModel::pflags)
     std::vector<int32_t> spos;    // decoded paths (BandModel::spos)
     uint32_t hx_exist = 0, hl_exist = 0;
+    bool ties_heavy = false;  // every light position has a heavy term that wins ties (BandModel)
     size_t lds_bytes = 0;
     // the decoded-path chain variant can run this plan
     bool paths_ok() const { return ok && chain && !ge && HA <= 1 && chain_paths_supported((int)SM, (int)(B / 64)); }
