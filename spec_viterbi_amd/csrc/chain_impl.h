@@ -115,25 +115,26 @@ __device__ __forceinline__ float row_min16(float x) {
     return x;
 }
 
-// acc = (acc << 1) | bit per lane: v_addc acc + acc + carry, the carry-in the 64-bit lane mask.
-// The mask reaches the VALU through an SALU instruction: read straight after the VALU compare
-// that wrote it, an SGPR operand came back stale on MI355X (hipcc pads no hazard for an asm
-// consumer).  push_bit: bit = lt | (eq & c); push_bit1: bit = m.
-__device__ __forceinline__ void push_bit(uint32_t& acc, uint64_t lt, uint64_t eq, uint64_t c) {
-    uint64_t k, co;
-    asm volatile("s_and_b64 %1, %4, %5\n\t"
-                 "s_or_b64 %1, %1, %3\n\t"
-                 "v_addc_co_u32_e64 %0, %2, %0, %0, %1"
-                 : "+v"(acc), "=&s"(k), "=&s"(co)
-                 : "s"(lt), "s"(eq), "s"(c)
-                 : "scc");
+// acc = (acc << 1) | bit per lane as v_addc_co_u32 acc, acc, acc with the compare's lane mask in
+// VCC as the carry-in (hipcc's own code for the same C is four VALU ops: compare, shift, select,
+// or).  push_le: bit = [x <= y]; push_lt_eqc: bit = [x < y] | (c & [x == y]), c a lane mask.
+__device__ __forceinline__ void push_le(uint32_t& acc, float x, float y) {
+    asm volatile("v_cmp_le_f32_e32 vcc, %1, %2\n\t"
+                 "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                 : "+v"(acc)
+                 : "v"(x), "v"(y)
+                 : "vcc");
 }
-__device__ __forceinline__ void push_bit1(uint32_t& acc, uint64_t m) {
-    uint64_t k, co;
-    asm volatile("s_mov_b64 %1, %3\n\t"
-                 "v_addc_co_u32_e64 %0, %2, %0, %0, %1"
-                 : "+v"(acc), "=&s"(k), "=&s"(co)
-                 : "s"(m));
+__device__ __forceinline__ void push_lt_eqc(uint32_t& acc, float x, float y, uint64_t c) {
+    uint64_t e;
+    asm volatile("v_cmp_eq_f32_e64 %1, %2, %3\n\t"
+                 "s_and_b64 %1, %1, %4\n\t"
+                 "v_cmp_lt_f32_e32 vcc, %2, %3\n\t"
+                 "s_or_b64 vcc, vcc, %1\n\t"
+                 "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                 : "+v"(acc), "=&s"(e)
+                 : "v"(x), "v"(y), "s"(c)
+                 : "vcc", "scc");
 }
 
 // f(integral_constant<int, I>) for I in [I0, N): a loop whose index is a constant expression
@@ -514,12 +515,10 @@ __global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, Fuse
                 const float xh = xa[0][s] + vh[0];
                 const float xbe = s == 0 ? xb0 : xb[s];
                 // heavy term taken: below the chain term, or tied and winning the tie
-                if constexpr (PATHS == 2) {
-                    push_bit1(macc[s], __builtin_amdgcn_ballot_w64(xh <= xbe));
-                } else {
-                    push_bit(macc[s], __builtin_amdgcn_ballot_w64(xh < xbe), __builtin_amdgcn_ballot_w64(xh == xbe),
-                             pmC[s]);
-                }
+                if constexpr (PATHS == 2)
+                    push_le(macc[s], xh, xbe);
+                else
+                    push_lt_eqc(macc[s], xh, xbe, pmC[s]);
             };
             StaticFor<0, SM>::run(mask_slot);
         }
