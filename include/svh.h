@@ -126,13 +126,16 @@ int svh_batch_create(svh_model_t m, uint64_t nseq, const uint64_t* offsets,
  * svh_spec_build(level)).  Paths need level <= 1 and SVH_BATCH_PATHS. */
 int svh_batch_run(svh_batch_t b, uint32_t level, void* stream);
 /* Opt-in time-parallel pass (scores only, level 0).  Sequences longer than
- * 2*seg_len are cut into segments of >= seg_len observations that all run at once from a guess;
- * segment k is then fixed up from the corrected end of k-1: a probe of probe_len observations from
- * that exact start, compared with the guess run's probe -- if they differ by a constant (within
- * rel_tol of the best score), the guess run's end plus that constant is taken, else the rest of
- * the segment is re-run exactly.  Scores match the serial pass up to rounding (not bit-exact);
- * rel_tol < 0 re-runs every segment (bit-exact, for verification).  *fallbacks (nullable) =
- * segments that were re-run.  Synchronous. */
+ * 2*seg_len are cut into equal segments of >= seg_len observations that all run at once from
+ * guesses: a light guess (zeros, heavy rows +inf) and, for chain/band models, one unit vector per
+ * heavy row.  Segment k is then fixed up on the device from the corrected end v of k-1: the
+ * heavy-row runs shifted by v's heavy scores are exact by (min,+)-linearity, and a probe of
+ * probe_len observations from v's light part is compared with the light guess's probe -- if they
+ * differ by a constant (within rel_tol of the best score) wherever the light part is not already
+ * dominated by the heavy-row terms, the light guess's end plus that constant is taken, else the
+ * rest of the segment is re-run exactly.  Scores match the serial pass up to rounding (not
+ * bit-exact); rel_tol < 0 re-runs every segment (bit-exact, for verification).  *fallbacks
+ * (nullable) = segments that were re-run.  Synchronous (one host wait at the end). */
 int svh_batch_run_time_parallel(svh_batch_t b, uint32_t seg_len, uint32_t probe_len, float rel_tol,
                                 void* stream, uint64_t* fallbacks);
 /* Synchronise `stream` and copy results to host (any pointer may be NULL). */

@@ -244,19 +244,34 @@ struct SpecChunkBatch {
 hipError_t launch_spec_chunk(const CsrModel& m, const float* products, const SpecChunkBatch& c,
                              uint32_t pstride, hipStream_t stream);
 // Time-parallel helpers (timepar.hip; Batch::run_time_parallel).  Row index tables per active
-// segment r: probe run from the exact start (x), from the guess (g), guess segment end (e),
-// destination row (out), probe covered the whole segment (full: out = X).
+// segment r: probe run from the exact start (x; the probe from the start's light part is row
+// x + xl_off), first of the segment's guess probe rows (g: the light guess, then one row per basis
+// row), first of its guess end rows (e, same order), destination row (out), probe covered the
+// whole segment (full: out = X), the probe's last step (pend) and the segment's (send).
 struct TpRows {
     const uint32_t* x;
     const uint32_t* g;
     const uint32_t* e;
     const uint32_t* out;
     const uint32_t* full;
+    const uint32_t* pend;
+    const uint32_t* send;
 };
+// Basis rows of the guess runs (the model's heavy rows, run from unit start vectors).
+struct TpBasis {
+    int32_t hrow[kBandHeavy];
+    uint32_t H;
+};
+// out[orow[r]] = in[irow[r]] (only where flag[r] != 0 when flag is given)
 hipError_t launch_tp_copy_rows(const float* in, const uint32_t* irow, float* out, const uint32_t* orow,
-                               uint32_t rows, uint32_t n, hipStream_t s);
+                               uint32_t rows, uint32_t n, const uint32_t* flag, hipStream_t s);
+// out rows [0, nseq): S; rows [nseq, 2 nseq): S with the basis rows at +inf (the light part).
+hipError_t launch_tp_probe_starts(const float* S, float* out, uint32_t nseq, uint32_t n, const TpBasis& basis,
+                                  hipStream_t s);
+// flag[r] = 1: not converged; the fallback row r runs steps fbeg[r]..fend[r]-1 (none when converged)
 hipError_t launch_tp_correct(const float* X, const float* G, const float* E1, const TpRows& rows, uint32_t count,
-                             float* out, uint32_t n, float tol, uint32_t* flag, hipStream_t s);
+                             uint32_t xl_off, const TpBasis& basis, float* out, uint32_t n, float tol,
+                             uint32_t* flag, uint32_t* fbeg, uint32_t* fend, hipStream_t s);
 hipError_t launch_tp_finish(const float* S, float* scores, int64_t* best, uint32_t nseq, uint32_t n, hipStream_t s);
 
 // v0[q][j] = fl(E[s0][j] + start[j]) for every sequence.

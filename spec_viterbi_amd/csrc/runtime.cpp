@@ -9,6 +9,7 @@
 #include <cstring>
 #include <limits>
 #include <map>
+#include <memory>
 #include <numeric>
 
 namespace svh {
@@ -1024,158 +1025,179 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
     uint32_t kmax = 1;
     for (uint32_t q = 0; q < nseq; ++q) {
         const uint32_t L = lens[q];
-        const uint32_t P = L > 2 * seg ? L / seg : 1;  // segments of seg..2*seg-1 observations
+        // P equal segments of at least seg observations (the longest bounds the parallel phase)
+        const uint32_t P = L > 2 * seg ? L / seg : 1;
         first_seg[q] = (uint32_t)segs.size();
         nsegs[q] = P;
         kmax = std::max(kmax, P);
-        for (uint32_t k = 0; k < P; ++k) segs.push_back({q, k, k * seg, k + 1 == P ? L : (k + 1) * seg});
+        for (uint32_t k = 0; k < P; ++k)
+            segs.push_back({q, k, (uint32_t)((uint64_t)k * L / P), (uint32_t)((uint64_t)(k + 1) * L / P)});
     }
     const uint32_t nv = (uint32_t)segs.size();
+    // basis rows: the heavy rows of the model's band plan (none for other models).  Every segment
+    // runs nb guesses: the light guess (zeros, basis rows +inf), then a unit vector per basis row.
+    TpBasis basis{};
+    if (const DeviceBandPlan* bpl = model->band_for(false))
+        for (int x = 0; x < kBandHeavy; ++x)
+            if (bpl->plan.hvalid[x]) basis.hrow[basis.H++] = bpl->plan.hrow[x];
+    const uint32_t nb = 1 + basis.H;
     // device scratch (freed at return)
-    DeviceBuffer d_zero, d_G, d_E1, d_X, d_S, d_Y, d_vbest, d_flag;
-    DeviceBuffer d_vsym, d_vbeg, d_vend, d_vrow, d_rows;
-    std::vector<float> zero(n, 0.0f);
-    d_zero.upload_async(zero.data(), (size_t)n * 4, s);
-    d_G.reserve((size_t)nv * n * 4);
-    d_E1.reserve((size_t)nv * n * 4);
-    d_X.reserve((size_t)nv * n * 4);
+    DeviceBuffer d_zero, d_G, d_E1, d_X, d_P, d_S, d_Y, d_vbest, d_flag;
+    std::vector<float> guess((size_t)nb * n, 0.0f);
+    for (uint32_t b = 0; b < basis.H; ++b) {
+        guess[basis.hrow[b]] = kInfH;
+        std::fill(guess.begin() + (size_t)(b + 1) * n, guess.begin() + (size_t)(b + 2) * n, kInfH);
+        guess[(size_t)(b + 1) * n + basis.hrow[b]] = 0.0f;
+    }
+    d_zero.upload_async(guess.data(), guess.size() * 4, s);
+    d_G.reserve((size_t)nv * nb * n * 4);
+    d_E1.reserve((size_t)nv * nb * n * 4);
+    d_X.reserve((size_t)2 * nv * n * 4);
+    d_P.reserve((size_t)2 * nseq * n * 4);
     d_S.reserve((size_t)nseq * n * 4);
     d_Y.reserve((size_t)nv * n * 4);
-    d_vbest.reserve((size_t)nv * 8);
-    d_flag.reserve((size_t)nv * 4);
-    // one launch of the step kernel over rows (begin, end, v_in row) of the batch's sequences
+    d_vbest.reserve((size_t)2 * nv * nb * 8);
+    // One launch of the step kernel over rows (begin, end, v_in row) of the batch's sequences.
+    // Nothing here waits for the device: every launch's row tables get device buffers of their
+    // own (sized up front, so none is reallocated under a pending kernel) and their host copies
+    // live until the end of the run; begin/end may instead come from the device (fallbacks).
+    std::vector<std::unique_ptr<DeviceBuffer>> dev_keep;
+    std::vector<std::vector<uint64_t>> host_keep64;
+    std::vector<std::vector<uint32_t>> host_keep32;
     std::vector<uint64_t> vsym;
     std::vector<uint32_t> vbeg, vend, vrow;
-    auto launch_rows = [&](const float* v_in, float* out) {
-        const uint32_t rows = (uint32_t)vbeg.size();
+    auto table32 = [&](std::vector<uint32_t>& v) -> const uint32_t* {
+        host_keep32.push_back(std::move(v));
+        v.clear();
+        dev_keep.push_back(std::make_unique<DeviceBuffer>());
+        dev_keep.back()->upload_async(host_keep32.back().data(), host_keep32.back().size() * 4, s);
+        return dev_keep.back()->as<uint32_t>();
+    };
+    auto launch_rows = [&](const float* v_in, float* out, const uint32_t* dbeg = nullptr,
+                           const uint32_t* dend = nullptr) {
+        const uint32_t rows = (uint32_t)vsym.size();
         if (rows == 0) return;
-        d_vsym.upload_async(vsym.data(), (size_t)rows * 8, s);
-        d_vbeg.upload_async(vbeg.data(), (size_t)rows * 4, s);
-        d_vend.upload_async(vend.data(), (size_t)rows * 4, s);
-        d_vrow.upload_async(vrow.data(), (size_t)rows * 4, s);
+        host_keep64.push_back(std::move(vsym));
+        vsym.clear();
+        dev_keep.push_back(std::make_unique<DeviceBuffer>());
+        dev_keep.back()->upload_async(host_keep64.back().data(), (size_t)rows * 8, s);
         FusedBatch fb;
         std::memset(&fb, 0, sizeof(fb));
         fb.symbols = d_sym.as<uint8_t>();
-        fb.sym_off = d_vsym.as<uint64_t>();
-        fb.begin = d_vbeg.as<uint32_t>();
-        fb.end = d_vend.as<uint32_t>();
+        fb.sym_off = dev_keep.back()->as<uint64_t>();
+        fb.begin = dbeg ? dbeg : table32(vbeg);
+        fb.end = dend ? dend : table32(vend);
         fb.v_in = v_in;
-        fb.v_in_row = d_vrow.as<uint32_t>();
+        fb.v_in_row = table32(vrow);
         fb.scores = out;
         fb.best = d_vbest.as<int64_t>();
         fb.nseq = rows;
-        model->launch_steps(fb, false, s);
-        // the host arrays are reused by the next launch: let this one's uploads land first
-        hip_check(hipStreamSynchronize(s), "time-parallel launch");
-    };
-    auto clear_rows = [&] {
-        vsym.clear();
         vbeg.clear();
         vend.clear();
-        vrow.clear();
+        model->launch_steps(fb, false, s);
     };
     hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
-    // 1a: probes from the guess (segment 0: from the start column)
-    clear_rows();
+    // 1a: probes from the guesses, rows v * nb + b (segment 0: from the start column, and its
+    // basis rows are unused zero-step copies)
     for (const Seg& x : segs) {
-        vsym.push_back(h_symoff[x.q]);
-        vbeg.push_back(x.k == 0 ? 0u : x.b);
-        vend.push_back(std::min(x.b + probe, x.e));
-        vrow.push_back(0);
+        for (uint32_t b = 0; b < nb; ++b) {
+            const bool unused = x.k == 0 && b > 0;
+            vsym.push_back(h_symoff[x.q]);
+            vbeg.push_back(unused ? 1u : x.k == 0 ? 0u : x.b);
+            vend.push_back(unused ? 1u : std::min(x.b + probe, x.e));
+            vrow.push_back(b);
+        }
     }
     launch_rows(d_zero.as<float>(), d_G.as<float>());
     // 1b: the rest of every segment (a zero-step row copies its start)
-    clear_rows();
     for (uint32_t v = 0; v < nv; ++v) {
         const Seg& x = segs[v];
-        vsym.push_back(h_symoff[x.q]);
-        vbeg.push_back(std::min(x.b + probe, x.e));
-        vend.push_back(x.e);
-        vrow.push_back(v);
+        for (uint32_t b = 0; b < nb; ++b) {
+            const bool unused = x.k == 0 && b > 0;
+            vsym.push_back(h_symoff[x.q]);
+            vbeg.push_back(unused ? 1u : std::min(x.b + probe, x.e));
+            vend.push_back(unused ? 1u : x.e);
+            vrow.push_back(v * nb + b);
+        }
     }
     launch_rows(d_G.as<float>(), d_E1.as<float>());
     // S[q] = end of segment 0 (exact)
     {
         std::vector<uint32_t> irow(nseq), orow(nseq);
         for (uint32_t q = 0; q < nseq; ++q) {
-            irow[q] = first_seg[q];
+            irow[q] = first_seg[q] * nb;
             orow[q] = q;
         }
-        d_rows.upload_async(irow.data(), (size_t)nseq * 4, s);
-        DeviceBuffer d_orow;
-        d_orow.upload_async(orow.data(), (size_t)nseq * 4, s);
-        hip_check(launch_tp_copy_rows(d_E1.as<float>(), d_rows.as<uint32_t>(), d_S.as<float>(), d_orow.as<uint32_t>(),
-                                      nseq, n, s),
+        const uint32_t* di = table32(irow);
+        const uint32_t* dout = table32(orow);
+        hip_check(launch_tp_copy_rows(d_E1.as<float>(), di, d_S.as<float>(), dout, nseq, n, nullptr, s),
                   "time-parallel copy");
-        hip_check(hipStreamSynchronize(s), "time-parallel copy");
     }
-    // 2: segments 1, 2, ... in order, all sequences at once
-    uint64_t nfall = 0;
-    DeviceBuffer d_rx, d_rg, d_re, d_ro, d_rf;
+    // 2: segments 1, 2, ... in order, all sequences at once.  The correction kernel decides on
+    // the device which segments are re-run: it writes each fallback row's (begin, end), a
+    // converged segment's row has no steps, and only flagged rows are copied into S.
+    uint32_t nflags = 0;
+    DeviceBuffer d_fbeg, d_fend;
+    d_fbeg.reserve((size_t)nv * 4);
+    d_fend.reserve((size_t)nv * 4);
+    d_flag.reserve((size_t)nv * 4);
     for (uint32_t k = 1; k < kmax; ++k) {
         std::vector<uint32_t> act;  // virtual segment ids of segment k
         for (uint32_t q = 0; q < nseq; ++q)
             if (nsegs[q] > k) act.push_back(first_seg[q] + k);
         if (act.empty()) break;
         const uint32_t na = (uint32_t)act.size();
-        // probe from the exact start S[q] -> X rows 0..na-1
-        clear_rows();
-        std::vector<uint32_t> rx(na), rg(na), re(na), ro(na), rf(na);
-        for (uint32_t a = 0; a < na; ++a) {
-            const Seg& x = segs[act[a]];
-            vsym.push_back(h_symoff[x.q]);
-            vbeg.push_back(x.b);
-            vend.push_back(std::min(x.b + probe, x.e));
-            vrow.push_back(x.q);
-            rx[a] = a;
-            rg[a] = act[a];
-            re[a] = act[a];
-            ro[a] = x.q;
-            rf[a] = x.b + probe >= x.e ? 1u : 0u;
+        // probes from the exact start S[q] -> X rows 0..na-1, and (with basis rows) from its light
+        // part -> X rows na..2na-1
+        hip_check(launch_tp_probe_starts(d_S.as<float>(), d_P.as<float>(), nseq, n, basis, s), "time-parallel starts");
+        std::vector<uint32_t> rx(na), rg(na), re(na), ro(na), rf(na), rp(na), rs(na);
+        for (uint32_t part = 0; part < (basis.H ? 2u : 1u); ++part) {
+            for (uint32_t a = 0; a < na; ++a) {
+                const Seg& x = segs[act[a]];
+                vsym.push_back(h_symoff[x.q]);
+                vbeg.push_back(x.b);
+                vend.push_back(std::min(x.b + probe, x.e));
+                vrow.push_back(part * nseq + x.q);
+                rx[a] = a;
+                rg[a] = act[a] * nb;
+                re[a] = act[a] * nb;
+                ro[a] = x.q;
+                rf[a] = x.b + probe >= x.e ? 1u : 0u;
+                rp[a] = std::min(x.b + probe, x.e);
+                rs[a] = x.e;
+            }
         }
-        launch_rows(d_S.as<float>(), d_X.as<float>());
-        d_rx.upload_async(rx.data(), (size_t)na * 4, s);
-        d_rg.upload_async(rg.data(), (size_t)na * 4, s);
-        d_re.upload_async(re.data(), (size_t)na * 4, s);
-        d_ro.upload_async(ro.data(), (size_t)na * 4, s);
-        d_rf.upload_async(rf.data(), (size_t)na * 4, s);
-        TpRows tr{d_rx.as<uint32_t>(), d_rg.as<uint32_t>(), d_re.as<uint32_t>(), d_ro.as<uint32_t>(),
-                  d_rf.as<uint32_t>()};
-        hip_check(launch_tp_correct(d_X.as<float>(), d_G.as<float>(), d_E1.as<float>(), tr, na, d_S.as<float>(), n,
-                                    tol, d_flag.as<uint32_t>(), s),
+        launch_rows(d_P.as<float>(), d_X.as<float>());
+        std::vector<uint32_t> ya(na);
+        for (uint32_t a = 0; a < na; ++a) ya[a] = a;
+        TpRows tr{table32(rx), table32(rg), table32(re), table32(ro), table32(rf), table32(rp), table32(rs)};
+        uint32_t* flag = d_flag.as<uint32_t>() + nflags;
+        hip_check(launch_tp_correct(d_X.as<float>(), d_G.as<float>(), d_E1.as<float>(), tr, na, basis.H ? na : 0,
+                                    basis, d_S.as<float>(), n, tol, flag, d_fbeg.as<uint32_t>(),
+                                    d_fend.as<uint32_t>(), s),
                   "time-parallel correction");
-        std::vector<uint32_t> flag(na);
-        hip_check(hipMemcpyAsync(flag.data(), d_flag.ptr, (size_t)na * 4, hipMemcpyDeviceToHost, s), "flags D2H");
-        hip_check(hipStreamSynchronize(s), "time-parallel flags");
-        // not converged: the rest of the segment from X, exactly, into Y, then into S
-        clear_rows();
-        std::vector<uint32_t> yi, yo;
+        // fallbacks: the rest of each flagged segment from X, exactly, into Y, then into S
         for (uint32_t a = 0; a < na; ++a) {
-            if (!flag[a]) continue;
             const Seg& x = segs[act[a]];
             vsym.push_back(h_symoff[x.q]);
-            vbeg.push_back(x.b + probe);
-            vend.push_back(x.e);
             vrow.push_back(a);
-            yi.push_back((uint32_t)yi.size());
-            yo.push_back(x.q);
         }
-        if (!yi.empty()) {
-            nfall += yi.size();
-            launch_rows(d_X.as<float>(), d_Y.as<float>());
-            d_rx.upload_async(yi.data(), yi.size() * 4, s);
-            d_ro.upload_async(yo.data(), yo.size() * 4, s);
-            hip_check(launch_tp_copy_rows(d_Y.as<float>(), d_rx.as<uint32_t>(), d_S.as<float>(), d_ro.as<uint32_t>(),
-                                          (uint32_t)yi.size(), n, s),
-                      "time-parallel copy");
-            hip_check(hipStreamSynchronize(s), "time-parallel fallback");
-        }
+        launch_rows(d_X.as<float>(), d_Y.as<float>(), d_fbeg.as<uint32_t>(), d_fend.as<uint32_t>());
+        const uint32_t* dya = table32(ya);
+        hip_check(launch_tp_copy_rows(d_Y.as<float>(), dya, d_S.as<float>(), tr.out, na, n, flag, s),
+                  "time-parallel copy");
+        nflags += na;
     }
     hip_check(launch_tp_finish(d_S.as<float>(), d_scores.as<float>(), d_best.as<int64_t>(), nseq, n, s),
               "time-parallel finish");
     hip_check(hipEventRecord(ev_stop, s), "hipEventRecord");
+    std::vector<uint32_t> flags(nflags);
+    if (nflags)
+        hip_check(hipMemcpyAsync(flags.data(), d_flag.ptr, (size_t)nflags * 4, hipMemcpyDeviceToHost, s), "flags D2H");
     hip_check(hipStreamSynchronize(s), "time-parallel run");
     model->check_fault();
+    uint64_t nfall = 0;
+    for (uint32_t f : flags) nfall += f;
     if (fallbacks) *fallbacks = nfall;
     ran = true;
 }
