@@ -25,6 +25,8 @@ def main(argv=None):
     p.add_argument("--paths", action="store_true")
     p.add_argument("--out", default="")
     p.add_argument("--backend", default="", help="nccl (default with GPUs) or gloo")
+    p.add_argument("--time-parallel", default="", metavar="SEG,PROBE",
+                   help="opt-in time-parallel pass per rank (scores only; DESIGN.md 6b), e.g. 1024,128")
     args = p.parse_args(argv)
 
     import torch
@@ -44,7 +46,9 @@ def main(argv=None):
         hmm = read_HMM(args.model)
         seqs = read_emit_seq(args.ess)
         device = f"cuda:{local}" if backend == "nccl" else None
-        scores, best, paths, secs = run_sharded(hmm, seqs, level=args.level, paths=args.paths, device=device)
+        tp = tuple(int(x) for x in args.time_parallel.split(",")) if args.time_parallel else None
+        scores, best, paths, secs = run_sharded(hmm, seqs, level=args.level, paths=args.paths, device=device,
+                                                time_parallel=tp)
         if dist.get_rank() == 0:
             updates = int(hmm.states_num) * sum(int(s.size) for s in seqs)
             print(json.dumps({"sequences": len(seqs), "states": int(hmm.states_num), "ranks": dist.get_world_size(),

@@ -86,19 +86,26 @@ def gather_paths(local_idx, local_paths, lengths, group=None, device=None):
     return [out[q, : int(lengths[q])].copy() for q in range(len(lengths))]
 
 
-def _hip_compute(device: int):
+def _hip_compute(device: int, time_parallel=None):
     """The product's shard compute: one DeviceModel batch on this rank's GPU (fails loudly
-    without the HIP library)."""
+    without the HIP library).  time_parallel = (seg_len, probe_len): the opt-in time-parallel
+    pass (scores only, level 0) -- a rank's makespan is otherwise its longest
+    sequence."""
     from .viterbi import DeviceModel
 
     def compute(hmm, seqs, level: int, paths: bool):
+        if time_parallel and (paths or level >= 2):
+            raise ValueError("time-parallel runs compute scores only at level 0/1")
         model = DeviceModel(hmm, device=device)
         try:
             if level >= 2:
                 model.spec_build(level)
             batch = model.batch(seqs, paths=paths)
             try:
-                batch.run(level)
+                if time_parallel:
+                    batch.run_time_parallel(seg_len=time_parallel[0], probe_len=time_parallel[1])
+                else:
+                    batch.run(level)
                 return batch.read(want_paths=paths)
             finally:
                 batch.close()
@@ -109,7 +116,7 @@ def _hip_compute(device: int):
 
 
 def run_sharded(hmm, seqs, *, level: int = 0, paths: bool = False, group=None, device=None,
-                compute=None):
+                compute=None, time_parallel=None):
     """Viterbi over `seqs` sharded across the ranks of `group` (torch.distributed, initialised).
 
     Each rank runs its LPT share with `compute(hmm, local_seqs, level, paths)` -- by default the
@@ -127,7 +134,7 @@ def run_sharded(hmm, seqs, *, level: int = 0, paths: bool = False, group=None, d
     mine = lpt_assign(lengths, world)[rank]
     if compute is None:
         index = torch.device(device).index if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
-        compute = _hip_compute(index or 0)
+        compute = _hip_compute(index or 0, time_parallel)
     n = int(hmm.states_num)
     dist.barrier(group)
     t0 = time.perf_counter()

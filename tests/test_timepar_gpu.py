@@ -94,3 +94,35 @@ def test_errors():
     with pytest.raises(_lib.SvhError) as e:
         model.batch(seqs).run_time_parallel(seg_len=100, probe_len=100)
     assert e.value.code == _lib.SVH_E_INVALID
+
+
+def test_sharded_runner_time_parallel():
+    """run_sharded(time_parallel=...) on one gloo rank: the rank's batch takes the time-parallel
+    pass (covid-19 on the Pfam model) and the gathered scores stay within tolerance."""
+    import socket
+
+    import torch.distributed as dist
+
+    from spec_viterbi_amd.sharding import run_sharded
+
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("covid-19.ess"))
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        scores, best, paths, secs = run_sharded(hmm, seqs, time_parallel=(1024, 128))
+    finally:
+        dist.destroy_process_group()
+    assert paths is None and secs > 0
+    for q, seq in enumerate(seqs):
+        ref = oracle.viterbi(hmm, seq)
+        assert close(scores[q], ref), q
+        assert best[q] == int(np.argmin(ref)), q
+    with pytest.raises(ValueError):
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        try:
+            run_sharded(hmm, seqs[:2], paths=True, time_parallel=(1024, 128))
+        finally:
+            dist.destroy_process_group()
