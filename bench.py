@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-check", action="store_true", help="skip the golden check (diagnostic ablations only)")
     p.add_argument("--paths", action="store_true", help="also decode paths (backpointers + traceback) every step")
+    p.add_argument("--replicate", type=int, default=1,
+                   help="batch = the file's sequences plus R-1 same-shape synthetic copies per GPU (full-chip "
+                        "weak scaling, SURVEY 8(e): emit_50 x 8k sequences = --replicate 160); 1 = the headline")
     return p.parse_args()
 
 
@@ -121,6 +124,10 @@ def main():
     else:  # same-shape synthetic batch per extra rank (weak scaling)
         rng = np.random.default_rng(rank)
         seqs = [rng.integers(0, hmm.emit_num, size=s.size).astype(np.uint64) for s in file_seqs]
+    if args.replicate > 1:
+        rng = np.random.default_rng(1000 + rank)
+        seqs = list(seqs) + [rng.integers(0, hmm.emit_num, size=s.size).astype(np.uint64)
+                             for _ in range(args.replicate - 1) for s in file_seqs]
     n = int(hmm.states_num)
     model = svh.DeviceModel(hmm, device=local, kernel=args.kernel, max_threads=args.max_threads)
     info = model.info()
@@ -204,7 +211,9 @@ def main():
             "data": "2405.chmm + emit_50_3500_20.ess (reference files) on rank 0; same-shape synthetic "
                     "sequences (numpy default_rng(rank)) on ranks > 0",
             "config": {
-                "workload": f"{args.model} x {args.ess}, " + (f"non-spec (min,+) step, {KERNEL_NAMES.get(info['kernel'], '?')} kernel" if args.level <= 1
+                "workload": f"{args.model} x {args.ess}" +
+                            (f" x{args.replicate} (file sequences + same-shape synthetic copies)" if args.replicate > 1 else "") +
+                            ", " + (f"non-spec (min,+) step, {KERNEL_NAMES.get(info['kernel'], '?')} kernel" if args.level <= 1
                                                               else f"_spec level {args.level}"),
                 "states": n, "nnz": nnz, "sequences_per_gpu": len(seqs), "observations_per_gpu": steps_obs,
                 "state_updates_per_gpu": updates_per_rank, "level": args.level,

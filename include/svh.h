@@ -104,7 +104,8 @@ typedef struct {
     uint64_t spec_level;   /* level of the products built by svh_spec_build (0/1: none needed) */
     uint64_t spec_bytes;   /* HBM held by the products */
     int32_t paths_kernel;  /* kernel of decoded-path runs (SVH_KERNEL_CHAIN, _FUSED or _GENERIC) */
-    int32_t reserved;
+    int32_t wide_threads;  /* chain plan for batches of more sequences than CUs (streamed E, more
+                              workgroups per CU): its threads per workgroup, 0 = none */
 } svh_model_info;
 int svh_model_get_info(svh_model_t m, svh_model_info* info);
 

@@ -46,7 +46,7 @@ class svh_model_info(ctypes.Structure):
         ("kernel", c_int32), ("family", c_int32), ("threads", c_int32), ("slots", c_int32),
         ("light_terms", c_int32), ("heavy_rows", c_int32), ("heavy_uniform", c_int32), ("device", c_int32),
         ("n", c_uint64), ("S", c_uint64), ("nnz", c_uint64), ("lds_bytes", c_uint64),
-        ("spec_level", c_uint64), ("spec_bytes", c_uint64), ("paths_kernel", c_int32), ("reserved", c_int32),
+        ("spec_level", c_uint64), ("spec_bytes", c_uint64), ("paths_kernel", c_int32), ("wide_threads", c_int32),
     ]
 
 

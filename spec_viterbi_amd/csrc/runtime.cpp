@@ -343,7 +343,7 @@ bool band_heavy_rows(const HostModel& hm, std::vector<uint32_t>* heavy_out) {
 
 }  // namespace
 
-BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
+BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge_waves) {
     BandPlan bp;
     const uint32_t n = hm.n, S = hm.S;
     if (chain && S > (uint32_t)kChainMaxSym) return bp;
@@ -421,9 +421,10 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain) {
 
     uint32_t SM = 0, B = 0;
     bool ge = false;
-    const char* ge_env = chain ? std::getenv("SVH_CHAIN_GE") : nullptr;  // diagnostic: waves
-    if (ge_env && std::atoi(ge_env) > 0) {
-        const uint32_t w = (uint32_t)std::atoi(ge_env);
+    const char* ge_env = std::getenv("SVH_CHAIN_GE");  // diagnostic: waves
+    const int gw = !chain ? 0 : ge_waves >= 0 ? ge_waves : (ge_env ? std::atoi(ge_env) : 0);
+    if (gw > 0) {
+        const uint32_t w = (uint32_t)gw;
         const uint32_t sm = (nL + 64 * w - 1) / (64 * w);
         if (chain_supported((int)sm, (int)w, (int)std::max<uint32_t>(HA, 1), true)) {
             SM = sm;
@@ -646,6 +647,15 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
             throw Error(SVH_E_UNSUPPORTED, "chain kernel requested but the model is not chain-shaped "
                                            "(or too large / too many symbols for it)");
         band.upload(bpl, host.n, host.S, stream);
+        // wide batches: the 8-wave E-in-VGPR geometry holds one workgroup per CU; 4 waves with
+        // streamed E fit two, which doubles throughput once every CU is busy
+        if (bpl.ok && bpl.chain && !bpl.ge && bpl.B >= 512) {
+            BandPlan wide = make_band_plan(host, 0, true, 4);
+            if (wide.ok) band_wide.upload(wide, host.n, host.S, stream);
+        }
+        int cus = 0;
+        hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device), "CU count");
+        cu_count = (uint32_t)cus;
     }
     Plan fast = make_plan(host, max_threads, true);
     fast_plan.upload(fast, stream);
@@ -702,11 +712,12 @@ CsrModel Model::csr_view() const {
     return c;
 }
 
-const DeviceBandPlan* Model::band_for(bool paths) const {
+const DeviceBandPlan* Model::band_for(bool paths, uint32_t nseq) const {
     if (!band.plan.ok) return nullptr;
     if (kernel_pref != SVH_KERNEL_AUTO && kernel_pref != SVH_KERNEL_BAND && kernel_pref != SVH_KERNEL_CHAIN)
         return nullptr;
     if (paths) return band.plan.paths_ok() ? &band : nullptr;  // decoded-path chain variant
+    if (band_wide.plan.ok && nseq > cu_count) return &band_wide;
     return &band;
 }
 
@@ -791,6 +802,7 @@ svh_model_info Model::info() const {
     i.spec_level = spec_level;
     i.spec_bytes = d_products.bytes;
     i.paths_kernel = band_for(true) ? SVH_KERNEL_CHAIN : plan_for(true) ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
+    i.wide_threads = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.B : 0;
     return i;
 }
 
@@ -1232,7 +1244,7 @@ void Batch::read_async(hipStream_t s, float* scores, int64_t* best, int32_t* pat
 // One pass of the per-observation step kernel over a batch view (steps begin..end-1 of each row).
 void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) const {
     const DevicePlan* dp = plan_for(want_paths);
-    const DeviceBandPlan* bpl = band_for(want_paths);
+    const DeviceBandPlan* bpl = band_for(want_paths, b.nseq);
     if (bpl) {
         const int ha = (int)std::max<uint32_t>(bpl->plan.HA, 1);
         if (bpl->plan.chain) hip_check(launch_chain(bpl->view, ha, b, s), "chain Viterbi kernel");
@@ -1250,9 +1262,10 @@ void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) co
 }
 
 void Model::check_fault() const {
-    if (band.plan.ok && band.view.fault) {
+    for (const DeviceBandPlan* p : {&band, &band_wide}) {
+        if (!p->plan.ok || !p->view.fault) continue;
         uint32_t fault = 0;
-        hip_check(hipMemcpy(&fault, band.view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
+        hip_check(hipMemcpy(&fault, p->view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
         if (fault) throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
     }
 }

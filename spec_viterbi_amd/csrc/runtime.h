@@ -112,7 +112,9 @@ struct BandPlan {
     // the decoded-path chain variant can run this plan
     bool paths_ok() const { return ok && chain && !ge && HA <= 1 && chain_paths_supported((int)SM, (int)(B / 64)); }
 };
-BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain);
+// ge_waves: -1 = SVH_CHAIN_GE (diagnostic) or none; 0 = none; w > 0 = streamed-E chain kernel
+// with w waves.
+BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge_waves = -1);
 
 struct DeviceBandPlan {
     BandPlan plan;
@@ -129,6 +131,9 @@ struct Model {
     HostModel host;
     hipStream_t stream = nullptr;
     DeviceBandPlan band;             // chain kernel plan (scores-only runs of MSV-shaped models)
+    DeviceBandPlan band_wide;        // chain plan for batches wider than the chip: streamed E,
+                                     // 4 waves (more workgroups per CU), scores only
+    uint32_t cu_count = 0;
     DevicePlan fast_plan;            // fastest fused plan (may use uniform heavy rows)
     DevicePlan paths_plan_storage;   // term-by-term plan when fast_plan is uniform
     const DevicePlan* paths_plan = nullptr;
@@ -143,8 +148,8 @@ struct Model {
     CsrModel csr_view() const;
     // Fused plan to run (nullptr: generic kernel).
     const DevicePlan* plan_for(bool paths) const;
-    // Chain plan to run for scores-only passes (nullptr: use plan_for(false)).
-    const DeviceBandPlan* band_for(bool paths) const;
+    // Chain plan to run for a pass over nseq sequences (nullptr: use plan_for(paths)).
+    const DeviceBandPlan* band_for(bool paths, uint32_t nseq = 0) const;
     void spec_build(uint32_t level, hipStream_t s);
     svh_model_info info() const;
     // throws if a chain-kernel bounded wait gave up since the model was created (synchronous)

@@ -326,3 +326,24 @@ def test_run_sharded_cli_covid_paths(tmp_path):
         assert bit_equal(res["scores"][q], sc), first_mismatch(res["scores"][q], sc)
         assert int(res["best"][q]) == best
         assert np.array_equal(res["paths"][offs[q]:offs[q + 1]], path)
+
+
+def test_wide_batch_streamed_plan_2405():
+    """A batch with more sequences than CUs runs the wide chain plan (4 waves, streamed E, two
+    workgroups per CU): bit-exact against the oracle, and against the same sequences run in
+    batches narrow enough for the default plan; its lengths cover 1, the 8-observation group
+    edges and the symbol-chunk refill."""
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    model = svh.DeviceModel(hmm)
+    info = model.info()
+    assert info["kernel"] == _lib.SVH_KERNEL_CHAIN and info["wide_threads"] == 256, info
+    rng = np.random.default_rng(11)
+    lens = [1, 2, 7, 8, 9, 15, 16, 17, 33] + list(rng.integers(1, 300, size=400))
+    seqs = [rng.integers(0, hmm.emit_num, size=int(k)).astype(np.uint64) for k in lens]
+    wide, wide_best = model.viterbi(seqs)
+    narrow = np.concatenate([model.viterbi(seqs[k:k + 100])[0] for k in range(0, len(seqs), 100)])
+    assert bit_equal(wide, narrow)
+    for q in list(range(9)) + [100, 257, len(seqs) - 1]:
+        ref = oracle.viterbi(hmm, seqs[q])
+        assert bit_equal(wide[q], ref), (q, first_mismatch(wide[q], ref))
+        assert wide_best[q] == int(np.argmin(ref)), q
