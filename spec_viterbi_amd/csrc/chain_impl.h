@@ -174,7 +174,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 //     (every kCkptEvery-th row of light scores, stored here) instead of this kernel finding j*
 //     for every observation (on 2405.chmm the path needs it about once per sequence).
 template <int SM, int W, int HA, bool GE, bool STAMP = false, int DIAG = 0, int PATHS = 0>
-__global__ __launch_bounds__(64 * W) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
+__global__ __launch_bounds__(64 * W, (GE && W == 4) ? 4 : 1) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
     static_assert(!PATHS || (HA == 1 && !GE && !STAMP && DIAG == 0), "decoded paths: HA 1, E in VGPRs");
     constexpr int HM = kBandHeavy;
     constexpr uint32_t B = 64 * W;
