@@ -1,22 +1,35 @@
 #!/usr/bin/env python3
 """Headline benchmark: M state-updates/s (states x observations / s) of the Viterbi hot path on
-2405.chmm x emit_50_3500_20.ess (BASELINE.json configs[2]), 1..N MI355X, weak scaling.
+2405.chmm x emit_50_3500_20.ess (BASELINE.json configs[2]), 1..N MI355X.
 
-One step = one pass of the fused (min,+) Viterbi kernel over the whole batch (50 sequences x
-3500 observations x 2407 states = 421,225,000 state-updates per GPU), inputs resident in HBM.
-Multi-GPU: one process per GPU (torchrun); every rank runs its own 50-sequence batch (rank 0 the
-reference file, rank r>0 same-shape synthetic sequences), no data-path collective; the timed
-region is bracketed by barrier + synchronize and the max over ranks is reported.
+One step = one pass of the (min,+) Viterbi step kernel over the whole batch (50 sequences x 3500
+observations x 2407 states = 421,225,000 state-updates per GPU), inputs resident in HBM.
 
-Prints ONE JSON line (rank 0).  Extra fields: roofline (dominant kernel, HIP-event timed on the
-stream it runs on) and cpu_baseline (the oracle, on this host's cores, bounded sample).
+Multi-GPU (one process per GPU): `--gpus N` without a torchrun environment re-launches this
+script under `torch.distributed.run` (a child process started before anything touches the GPU)
+and exits with its code; under torchrun WORLD_SIZE must equal N.
+  * default (`--shard none`, weak scaling): every rank runs its own 50-sequence batch (rank 0 the
+    reference file, rank r > 0 same-shape synthetic sequences), no data-path collective;
+  * `--shard covid` (strong scaling, BASELINE config 5): the 16 sequences of covid-19.ess are
+    LPT-assigned to the ranks (spec_viterbi_amd.sharding), each rank runs its share, and the
+    scores are gathered to rank 0 with one RCCL gather after the timed region.
+The timed region is bracketed by barrier + synchronize on every rank, the max over ranks is
+reported, and value = state-updates of all ranks / that time.
+
+Rank 0 prints ONE JSON line.  Extra objects: `roofline` (the dominant kernel: HIP-event time on
+the stream it runs on; VALU-issue utilisation and HBM bytes from rocprofv3 PMC passes this script
+runs as child processes on tools/launch.py with the same workload), `timing` (setup-inclusive and
+host-to-host rates) and `cpu_baseline` (the oracle on this host's cores).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -25,11 +38,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 DATA = os.path.join(ROOT, "data")
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CLOCK_GHZ = 2.4         # MI355X_MICROARCH.md: max shader clock
 KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain"}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -37,18 +51,78 @@ def parse():
     p.add_argument("--level", type=int, default=0, help="0 = non-spec (headline); >=2 = _spec path")
     p.add_argument("--model", default="2405.chmm")
     p.add_argument("--ess", default="emit_50_3500_20.ess")
+    p.add_argument("--shard", default="none", choices=["none", "covid"],
+                   help="none: weak scaling (a batch per rank); covid: strong scaling of 2405 x covid-19.ess")
     p.add_argument("--kernel", type=int, default=0, help="0 auto, 1 fused, 2 generic")
     p.add_argument("--max-threads", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC child passes")
     p.add_argument("--no-check", action="store_true", help="skip the golden check (diagnostic ablations only)")
     p.add_argument("--paths", action="store_true", help="also decode paths (backpointers + traceback) every step")
     p.add_argument("--replicate", type=int, default=1,
                    help="batch = the file's sequences plus R-1 same-shape synthetic copies per GPU (full-chip "
                         "weak scaling, SURVEY 8(e): emit_50 x 8k sequences = --replicate 160); 1 = the headline")
-    return p.parse_args()
+    p.add_argument("--dry-run", action="store_true",
+                   help="no GPU: exercise the launcher / rendezvous / timing scaffolding over gloo (CPU tests)")
+    return p.parse_args(argv)
 
 
+# ---- multi-process launch ----------------------------------------------------------------------
+def relaunch_under_torchrun(args, argv) -> int:
+    """`--gpus N` outside torchrun: start torch.distributed.run as a child (nothing here has
+    touched the GPU) with N ranks on 127.0.0.1, return its exit code."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
+def dist_setup(args):
+    """(world, rank, local) from the torchrun environment; process group initialised for N > 1."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if not args.dry_run:
+        import torch
+
+        torch.cuda.set_device(local)  # before the RCCL communicator is created
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo" if args.dry_run else "nccl", init_method="env://")
+    return world, rank, local
+
+
+def barrier(world, args):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+    if not args.dry_run:
+        import torch
+
+        torch.cuda.synchronize()
+
+
+def max_over_ranks(x: float, world, local, args) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if args.dry_run else f"cuda:{local}")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ---- accounting --------------------------------------------------------------------------------
 def algorithmic_bytes_per_step(n: int, nnz: int) -> int:
     """streamed-CSR bytes of one observation of one sequence:
     8*nnz (value + index) + 4*(n+1) (row pointers) + 4n (emission row) + 4n (read v) + 4n (write v)."""
@@ -56,10 +130,10 @@ def algorithmic_bytes_per_step(n: int, nnz: int) -> int:
 
 
 def algorithmic_bytes_per_launch(n: int, nnz: int, lengths, level: int, paths: bool) -> int:
-    """Bytes one launch must move under SURVEY.md 8(d)'s model, per sequence of length L:
-    level <= 1: (L-1) streamed-CSR steps (+ 2n uint16 backpointers per step and 4 B per path entry
-    with paths); level >= 2: floor((L-1)/level) dense products (4*n*round_up(n,4) + 8n each, the
-    product is read whole) plus the (L-1) % level tail steps streamed-CSR."""
+    """Bytes one launch must move under SURVEY.md 8(d)'s streamed-CSR model, per sequence of length
+    L: level <= 1: (L-1) steps (+ 2n uint16 backpointers per step and 4 B per path entry with
+    paths); level >= 2: floor((L-1)/level) dense products (4*n*round_up(n,4) + 8n each, read
+    whole) plus the (L-1) % level tail steps."""
     step = algorithmic_bytes_per_step(n, nnz)
     total = 0
     for L in lengths:
@@ -69,66 +143,194 @@ def algorithmic_bytes_per_launch(n: int, nnz: int, lengths, level: int, paths: b
         else:
             total += (L - 1) * step
             if paths:
-                total += (L - 1) * 2 * n * 2 + 4 * L  # backpointers written and read back, path
+                total += (L - 1) * 2 * n * 2 + 4 * L
     return total
 
 
+def host_cpu_info() -> dict:
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_cpus": None,
+            "model": None}
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            info["cgroup_cpus"] = round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if line.startswith("Model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
+
+
 def cpu_baseline(hmm, seqs, seconds: float) -> dict:
-    """The oracle (C restatement of GraphBLAS_impl, -O2, OpenMP over sequences) on this host."""
+    """The oracle (C restatement of GraphBLAS_impl, -O2, OpenMP over sequences) on this host:
+    all usable cores (CPU affinity, capped by the cgroup quota and by OMP_NUM_THREADS) over the
+    full batch, median of passes for ~`seconds`; then 1 thread over the full batch once."""
     from oracle import oracle
 
+    host = host_cpu_info()
+    usable = host["affinity"]
+    if host["cgroup_cpus"]:
+        usable = min(usable, max(1, int(host["cgroup_cpus"])))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        usable = min(usable, int(os.environ["OMP_NUM_THREADS"]))
     n = hmm.states_num
-    threads = min(16, os.cpu_count() or 1)
     work = n * sum(int(s.size) for s in seqs)
-    # multi-threaded passes over the whole batch, repeated for ~`seconds`
-    times = []
+    times, used = [], 1
     t_end = time.perf_counter() + seconds
-    used = 1
     while time.perf_counter() < t_end or not times:
         t0 = time.perf_counter()
-        _, used = oracle.viterbi_batch(hmm, seqs, nthreads=threads)
+        _, used = oracle.viterbi_batch(hmm, seqs, nthreads=usable)
         times.append(time.perf_counter() - t0)
     med = float(np.median(times))
-    # single-thread rate on a 4-sequence sample
-    sample = seqs[:4]
     t0 = time.perf_counter()
-    oracle.viterbi_batch(hmm, sample, nthreads=1)
+    oracle.viterbi_batch(hmm, seqs, nthreads=1)
     t1 = time.perf_counter() - t0
-    single = n * sum(int(s.size) for s in sample) / t1 / 1e6
     return {
         "value": round(work / med / 1e6, 2), "unit": "M state-updates/s", "cores": int(used), "kind": "port",
-        "sample": f"oracle/viterbi_oracle.c (GraphBLAS_impl restatement) over the full {len(seqs)}-sequence "
-                  f"batch, median of {len(times)} passes on {used} OpenMP threads; 1 thread: {single:.1f} M/s "
-                  f"on 4 sequences; host {os.cpu_count()} CPUs visible",
+        "one_thread": round(work / t1 / 1e6, 2),
+        "sample": f"oracle/viterbi_oracle.c (GraphBLAS_impl restatement, -O2) over the full {len(seqs)}-sequence "
+                  f"batch: median of {len(times)} passes on {used} OpenMP threads (usable cores); 1 thread: "
+                  f"{work / t1 / 1e6:.1f} M/s over the same batch ({t1:.2f} s)",
+        "host": host,
     }
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+# ---- rocprofv3 PMC passes (children on tools/launch.py) ---------------------------------------
+PMC_PASSES = {
+    "sq": ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY",
+           "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE"],
+    "fetch": ["FETCH_SIZE"],
+    "write": ["WRITE_SIZE"],
+}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
+
+def pmc_counters(launch_args: list[str], kernel_prefix: str) -> dict | None:
+    """Per-launch counters of the dominant kernel from separate rocprofv3 --pmc passes over
+    tools/launch.py (same workload), or None when rocprofv3 is unavailable or a pass fails."""
+    import csv
+    import glob
+
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None
+    out: dict[str, float] = {}
+    with tempfile.TemporaryDirectory(prefix="svh_pmc_") as d:
+        for name, counters in PMC_PASSES.items():
+            cmd = ["timeout", "-s", "KILL", "120", prof, "--pmc", *counters, "-f", "csv", "-d", os.path.join(d, name),
+                   "-o", "run", "--", sys.executable, os.path.join(ROOT, "tools", "launch.py"), *launch_args]
+            r = subprocess.run(cmd, capture_output=True, text=True, env=dict(os.environ, TMPDIR="/tmp"))
+            if r.returncode != 0:
+                sys.stderr.write(f"bench.py: rocprofv3 pass {name} failed ({r.returncode}): {r.stderr[-500:]}\n")
+                return None
+            per: dict[str, dict] = {}
+            for f in glob.glob(os.path.join(d, name, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        if not row.get("Kernel_Name", "").startswith(kernel_prefix):
+                            continue
+                        per.setdefault(row["Counter_Name"], {}).setdefault(row["Dispatch_Id"], 0.0)
+                        per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"] or 0)
+            for c, disp in per.items():
+                out[c] = sum(disp.values()) / len(disp)
+    return out or None
+
+
+def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc) -> dict:
+    """VALU-issue roofline of the chain kernel (the per-observation step is VALU + LDS work on
+    registers; HBM carries only symbols in and scores out).  Capacity of one SIMD-32: one wave64
+    VALU instruction per 2 cycles, and at most one per 4 cycles from a single wave
+    (MI355X_MICROARCH.md, cycle constants), so a SIMD holding w waves issues min(w/4, 1/2) per
+    cycle.  Peak = the SIMDs the launch occupies x that rate x 2.4 GHz; achieved = SQ_INSTS_VALU
+    per launch / HIP-event kernel time."""
+    waves_per_wg = max(1, int(plan["threads"]) // 64)
+    wide = plan["threads"] == info.get("wide_threads") and plan["slots"] == info.get("wide_slots") and nseq > info["cu_count"]
+    wg_per_cu = 4 if wide else 1  # launch-bounds occupancy of the wide plan; one WG per CU otherwise
+    cus = min(info["cu_count"], -(-nseq // wg_per_cu)) if info["cu_count"] else 256
+    waves_per_simd = min(8, waves_per_wg * min(wg_per_cu, -(-nseq // max(cus, 1))) / 4.0)
+    rate = min(waves_per_simd / 4.0, 0.5)  # wave-instructions per cycle per SIMD
+    peak = cus * 4 * rate * CLOCK_GHZ  # G wave-instructions / s
+    res = {"bound": "valu_issue", "unit": "G VALU wave-instr/s", "peak": round(peak, 2),
+           "achieved": None, "frac": None, "traffic": None, "kernel_ms": round(kernel_ms, 4),
+           "occupancy": {"cus": cus, "of_cus": info["cu_count"], "waves_per_simd": waves_per_simd,
+                         "workgroups_per_cu": wg_per_cu}}
+    gbs = algo_bytes / (kernel_ms * 1e-3) / 1e9
+    res["hbm"] = {"algorithmic_bytes": int(algo_bytes), "algorithmic_GBps": round(gbs, 1),
+                  "algorithmic_frac": round(gbs / HBM_PEAK_GBS, 4), "peak_GBps": HBM_PEAK_GBS,
+                  "measured_bytes": None, "measured_GBps": None, "measured_frac": None}
+    if pmc and "SQ_INSTS_VALU" in pmc:
+        ach = pmc["SQ_INSTS_VALU"] / (kernel_ms * 1e-3) / 1e9
+        res["achieved"] = round(ach, 2)
+        res["frac"] = round(ach / peak, 4)
+        res["valu_per_wave"] = round(pmc["SQ_INSTS_VALU"] / max(pmc.get("SQ_WAVES", 1), 1), 1)
+        if "SQ_WAVE_CYCLES" in pmc and "SQ_WAVES" in pmc:  # quad-cycles
+            res["wave_cycles"] = round(4 * pmc["SQ_WAVE_CYCLES"] / pmc["SQ_WAVES"], 0)
+            res["wait_frac"] = round(pmc.get("SQ_WAIT_ANY", 0) / pmc["SQ_WAVE_CYCLES"], 4)
+        if "GRBM_GUI_ACTIVE" in pmc:
+            res["profiled_clock_ghz"] = round(pmc["GRBM_GUI_ACTIVE"] / 8 / (kernel_ms * 1e6), 3)
+    if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:  # KiB; FETCH_SIZE doubled on gfx950
+        traffic = 2.0 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024
+        res["traffic"] = round(traffic)
+        mg = traffic / (kernel_ms * 1e-3) / 1e9
+        res["hbm"].update(measured_bytes=round(traffic), measured_GBps=round(mg, 2),
+                          measured_frac=round(mg / HBM_PEAK_GBS, 6))
+    res["note"] = ("frac = VALU wave-instructions issued (rocprofv3 SQ_INSTS_VALU, child pass on tools/launch.py) / "
+                   "kernel time, over the issue capacity of the CUs the launch occupies at 2.4 GHz; hbm.algorithmic_* "
+                   "is SURVEY 8(d)'s streamed-CSR model (47.98 B/state-update; the kernel keeps the model on chip, so it "
+                   "is not a bound), hbm.measured_* the PMC bytes (FETCH_SIZE x2 + WRITE_SIZE)")
+    return res
+
+
+# ---- workloads ---------------------------------------------------------------------------------
+def synthetic_like(seqs, S, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(0, S, size=s.size).astype(np.uint64) for s in seqs]
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return relaunch_under_torchrun(args, argv)
+    world, rank, local = dist_setup(args)
+    if args.dry_run:
+        return dry_run(args, world, rank, local)
+
+    import torch
 
     import spec_viterbi_amd as svh
+    from spec_viterbi_amd.sharding import gather_scores, lpt_assign
 
     hmm = svh.read_HMM(os.path.join(DATA, "chmm_files", args.model))
-    file_seqs = svh.read_emit_seq(os.path.join(DATA, "ess_files", args.ess))
-    if rank == 0:
-        seqs = file_seqs
-    else:  # same-shape synthetic batch per extra rank (weak scaling)
-        rng = np.random.default_rng(rank)
-        seqs = [rng.integers(0, hmm.emit_num, size=s.size).astype(np.uint64) for s in file_seqs]
+    ess_name = "covid-19.ess" if args.shard == "covid" else args.ess
+    file_seqs = svh.read_emit_seq(os.path.join(DATA, "ess_files", ess_name))
+    assignment = None
+    if args.shard == "covid":  # strong scaling: this rank's LPT share of the file
+        assignment = lpt_assign([s.size for s in file_seqs], world)
+        seqs = [file_seqs[q] for q in assignment[rank]]
+        data = f"{args.model} + covid-19.ess (reference files), LPT-sharded over {world} rank(s)"
+    else:
+        seqs = file_seqs if rank == 0 else synthetic_like(file_seqs, hmm.emit_num, rank)
+        data = (f"{args.model} + {ess_name} (reference files) on rank 0" +
+                ("; same-shape synthetic sequences (numpy default_rng(rank)) on ranks > 0" if world > 1 else ""))
     if args.replicate > 1:
         rng = np.random.default_rng(1000 + rank)
         seqs = list(seqs) + [rng.integers(0, hmm.emit_num, size=s.size).astype(np.uint64)
                              for _ in range(args.replicate - 1) for s in file_seqs]
+        data += f"; + {args.replicate - 1} same-shape synthetic copies per rank"
     n = int(hmm.states_num)
+
+    # setup (svh_model_create: host CSR + plans + upload), the counterpart of the per-call model
+    # build the reference times inside run_Viterbi (bench_Viterbi.h:53-56, GraphBLAS_impl.cpp:9-54)
+    setup = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        m = svh.DeviceModel(hmm, device=local, kernel=args.kernel, max_threads=args.max_threads)
+        setup.append(time.perf_counter() - t0)
+        m.close()
     model = svh.DeviceModel(hmm, device=local, kernel=args.kernel, max_threads=args.max_threads)
     info = model.info()
     prep_s = None
@@ -138,7 +340,8 @@ def main():
         model.spec_build(args.level)
         torch.cuda.synchronize()
         prep_s = time.perf_counter() - t_prep
-    batch = model.batch(seqs, paths=args.paths)
+    batch = model.batch(seqs, paths=args.paths) if seqs else None
+    plan = batch.plan(args.level) if batch else info
     # A stream of our own: torch's default stream has handle 0, which the C ABI reads as "the
     # model's own stream", so events recorded on torch's default stream would not bracket the
     # kernel.  Every launch and every event below goes to this one stream.
@@ -147,57 +350,79 @@ def main():
     assert sptr, "expected a non-null HIP stream handle"
 
     for _ in range(args.warmup):
-        batch.run(args.level, sptr)
+        if batch:
+            batch.run(args.level, sptr)
     torch.cuda.synchronize()
 
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     stops = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    barrier(world, args)
     t0 = time.perf_counter()
     for k in range(args.steps):
         starts[k].record(stream)
-        batch.run(args.level, sptr)
+        if batch:
+            batch.run(args.level, sptr)
         stops[k].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    barrier(world, args)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, local, args)
     kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, stops)]))
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-
-    # correctness guard on the timed output (rank 0 vs the committed golden of sequences 0..1)
-    if (rank == 0 and not args.no_check and args.level <= 1 and args.model == "2405.chmm"
-            and args.ess == "emit_50_3500_20.ess"):
+    scores = batch.read(sptr)[0] if batch else np.zeros((0, n), np.float32)
+    # correctness guard on the timed output (rank 0 vs the committed goldens of sequences 0..1)
+    golden_checked = False
+    if (rank == 0 and not args.no_check and args.shard == "none" and args.model == "2405.chmm"
+            and args.ess == "emit_50_3500_20.ess" and args.level <= 2):
         from tests.helpers import bit_equal, from_hex, load_golden
 
-        scores, _ = batch.read(sptr)
-        g = load_golden("chmm2405_emit50")
-        for rec in g["sequences"]:
-            assert bit_equal(scores[rec["index"]], from_hex(rec["scores"])), "bench output != golden"
+        for rec in load_golden("chmm2405_emit50")["sequences"]:
+            ref = rec["scores"] if args.level <= 1 else rec["spec"][str(args.level)]
+            assert bit_equal(scores[rec["index"]], from_hex(ref)), "bench output != golden"
+        golden_checked = True
+    gathered = None
+    if args.shard == "covid" and world > 1:  # one RCCL gather of the scores to rank 0
+        t_g = time.perf_counter()
+        gathered = gather_scores(assignment, scores, len(file_seqs), n, device=f"cuda:{local}")
+        gather_ms = (time.perf_counter() - t_g) * 1e3
 
-    updates_per_rank = n * sum(int(s.size) for s in seqs)
-    total_updates = updates_per_rank * world
+    if args.shard == "covid":
+        total_updates = n * sum(int(s.size) for s in file_seqs)
+        updates_per_rank = n * sum(int(s.size) for s in seqs)
+    else:
+        updates_per_rank = n * sum(int(s.size) for s in seqs)
+        total_updates = updates_per_rank * world
     value = total_updates * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
 
+    # host-to-host (svh_viterbi: symbols H2D, run, scores D2H), rank 0 only, after the timed region
+    e2e_ms = None
+    if rank == 0 and seqs:
+        e2e = []
+        for _ in range(5):
+            t_e = time.perf_counter()
+            model.viterbi(seqs, level=args.level)
+            e2e.append(time.perf_counter() - t_e)
+        e2e_ms = float(np.median(e2e)) * 1e3
+
     if rank == 0:
         nnz = int(info["nnz"])
-        steps_obs = sum(int(s.size) for s in seqs)
-        algo = algorithmic_bytes_per_launch(n, nnz, [int(x.size) for x in seqs], args.level, args.paths)
-        achieved = algo / (kernel_ms * 1e-3) / 1e9
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path) and args.level <= 1:
-            with open(pmc_path) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+        lengths = [int(x.size) for x in seqs]
+        algo = algorithmic_bytes_per_launch(n, nnz, lengths, args.level, args.paths)
+        kname = (KERNEL_NAMES.get(info["paths_kernel"], "?") + "+traceback" if args.paths
+                 else "spec_chunk+" + KERNEL_NAMES.get(plan["kernel"], "?") if args.level >= 2
+                 else KERNEL_NAMES.get(plan["kernel"], "?"))
+        pmc = None
+        if not args.no_pmc and world == 1 and args.level <= 1 and not args.paths and plan["kernel"] == 4:
+            largs = ["--model", args.model, "--ess", ess_name, "--replicate", str(args.replicate), "--steps", "3",
+                     "--warmup", "1"]
+            pmc = pmc_counters(largs, "void svh::(anonymous namespace)::chain_viterbi_kernel")
+        rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc)
+        workload = (f"{args.model} x {ess_name}" +
+                    (f" x{args.replicate} (file sequences + same-shape synthetic copies)" if args.replicate > 1 else "") +
+                    (", LPT-sharded (strong scaling)" if args.shard == "covid" else "") + ", " +
+                    (f"non-spec (min,+) step, {kname} kernel" if args.level <= 1 else f"_spec level {args.level}"))
         out = {
-            "metric": f"M state-updates/sec (states x obs/s) on {args.model} x {args.ess}",
+            "metric": f"M state-updates/sec (states x obs/s) on {args.model} x {ess_name}",
             "value": round(value, 2),
             "unit": "M state-updates/s",
             "n_gpus": world,
@@ -205,41 +430,66 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.shard == "covid" else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "2405.chmm + emit_50_3500_20.ess (reference files) on rank 0; same-shape synthetic "
-                    "sequences (numpy default_rng(rank)) on ranks > 0",
+            "data": data,
             "config": {
-                "workload": f"{args.model} x {args.ess}" +
-                            (f" x{args.replicate} (file sequences + same-shape synthetic copies)" if args.replicate > 1 else "") +
-                            ", " + (f"non-spec (min,+) step, {KERNEL_NAMES.get(info['kernel'], '?')} kernel" if args.level <= 1
-                                                              else f"_spec level {args.level}"),
-                "states": n, "nnz": nnz, "sequences_per_gpu": len(seqs), "observations_per_gpu": steps_obs,
-                "state_updates_per_gpu": updates_per_rank, "level": args.level,
-                "kernel": (KERNEL_NAMES.get(info["paths_kernel"], "?") + "+traceback" if args.paths
-                           else KERNEL_NAMES.get(info["kernel"], "?")),
-                "paths": bool(args.paths), "spec_prep_s": None if prep_s is None else round(prep_s, 4), "threads": info["threads"],
-                "slots": info["slots"], "heavy_rows": info["heavy_rows"], "heavy_uniform": info["heavy_uniform"],
-                "parallelism": f"sequence-sharded x{world} (one process per GPU, no collective)",
+                "workload": workload, "states": n, "nnz": nnz, "sequences_per_gpu": len(seqs),
+                "observations_per_gpu": sum(lengths), "state_updates_per_gpu": updates_per_rank, "level": args.level,
+                "kernel": kname, "threads": plan["threads"], "slots": plan["slots"], "paths": bool(args.paths),
+                "heavy_rows": plan["heavy_rows"], "spec_prep_s": None if prep_s is None else round(prep_s, 4),
+                "golden_checked": golden_checked,
+                "parallelism": (f"LPT sequence shards x{world}, one RCCL gather of scores after timing" if args.shard == "covid"
+                                else f"sequence-sharded x{world} (one process per GPU, no collective)"),
             },
-            "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "timing": {
                 "kernel_ms": round(kernel_ms, 4),
-                "note": "achieved = SURVEY 8(d) algorithmic bytes (47.98 B/state-update streamed-CSR model) / "
-                        "HIP-event kernel time; the kernel keeps T^T in VGPRs and v in LDS, so it is on-chip "
-                        "latency bound and frac > 1 is expected; traffic = PMC HBM bytes per launch",
+                "setup_ms": round(float(np.median(setup)) * 1e3, 3),
+                "e2e_ms_per_step": None if e2e_ms is None else round(e2e_ms, 3),
+                "e2e_M_state_updates_per_s": None if not e2e_ms else round(updates_per_rank / e2e_ms / 1e3, 2),
+                "setup_plus_e2e_M_state_updates_per_s": None if not e2e_ms else
+                round(updates_per_rank / (e2e_ms + float(np.median(setup)) * 1e3) / 1e3, 2),
+                "gather_ms": round(gather_ms, 3) if gathered is not None else None,
+                "note": "setup_ms = svh_model_create (host CSR + plans + upload; the reference rebuilds its model inside "
+                        "every run_Viterbi call, bench_Viterbi.h:53-56); e2e = svh_viterbi host symbols -> host scores "
+                        "(batch upload, run, D2H), median of 5 on rank 0",
             },
+            "roofline": rl,
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.level <= 1:
             out["cpu_baseline"] = cpu_baseline(hmm, file_seqs, args.cpu_seconds)
         print(json.dumps(out), flush=True)
-    batch.close()
+    if batch:
+        batch.close()
     model.close()
     if world > 1:
+        import torch.distributed as dist
+
         dist.destroy_process_group()
+    return 0
+
+
+def dry_run(args, world, rank, local) -> int:
+    """The launcher / rendezvous / barrier / max-over-ranks path with a fixed sleep as the step
+    (no GPU): rank r 'runs' for (r+1) ms per step, so the max over ranks is the last rank's."""
+    for _ in range(args.warmup):
+        time.sleep(0.001)
+    barrier(world, args)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001 * (rank + 1))
+    barrier(world, args)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, local, args)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": round(world * args.steps / elapsed, 3), "n_gpus": world,
+                          "steps": args.steps, "ms_per_step": round(elapsed / args.steps * 1e3, 4)}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

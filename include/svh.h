@@ -106,7 +106,10 @@ typedef struct {
     int32_t paths_kernel;  /* kernel of decoded-path runs (SVH_KERNEL_CHAIN, _FUSED or _GENERIC) */
     int32_t wide_threads;  /* chain plan for batches of more sequences than CUs (streamed E, more
                               workgroups per CU): its threads per workgroup, 0 = none */
+    int32_t wide_slots;    /* ... and its states per thread */
+    uint32_t cu_count;     /* CUs of the model's device: batches of more sequences switch plans */
 } svh_model_info;
+/* The model's plan for a one-sequence scores-only run (kernel/threads/slots describe it). */
 int svh_model_get_info(svh_model_t m, svh_model_info* info);
 
 /* ---- _spec: precomputed products of `level` consecutive observations ------------------- */
@@ -146,6 +149,9 @@ int svh_batch_read(svh_batch_t b, void* stream, float* scores /* nseq * n */,
 int svh_batch_device_results(svh_batch_t b, float** scores, int64_t** best_state);
 /* Milliseconds between the start and stop events of the last svh_batch_run (synchronises). */
 int svh_batch_elapsed_ms(svh_batch_t b, float* ms);
+/* The plan svh_batch_run(level) launches for this batch (its sequence count and paths flag
+ * decide between the narrow and the wide chain plan): kernel/threads/slots of the model info. */
+int svh_batch_plan(svh_batch_t b, uint32_t level, svh_model_info* info);
 int svh_batch_destroy(svh_batch_t b);
 
 /* Batch from uint8 symbols (the device format; e.g. straight from svh_reader_next). */

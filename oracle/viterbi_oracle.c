@@ -291,6 +291,8 @@ int ora_spec_products(const ora_hmm* h, uint32_t level, float* out) {
             return ORA_ENOMEM;
         }
         memcpy(tmp, out, prev_keys * nn * sizeof(float));
+        /* keys are independent: OpenMP over them (each product is computed exactly as above) */
+#pragma omp parallel for schedule(dynamic, 1) collapse(2)
         for (uint64_t k = 0; k < prev_keys; ++k)
             for (uint64_t i = 0; i < h->S; ++i)
                 left_multiply(h, &c, i, tmp + k * nn, out + (k * h->S + i) * nn);
@@ -333,6 +335,7 @@ int ora_viterbi_spec(const ora_hmm* h, uint32_t level, const uint64_t* seq, uint
             uint64_t key = 0;
             for (uint32_t q = 0; q < level; ++q, ++i) key = key * h->S + seq[i];
             const float* H = prod + key * n * n;
+#pragma omp parallel for schedule(static)
             for (uint64_t j = 0; j < n; ++j) {
                 float best = INFINITY;
                 for (uint64_t m = 0; m < n; ++m) {

@@ -174,7 +174,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 //     (every kCkptEvery-th row of light scores, stored here) instead of this kernel finding j*
 //     for every observation (on 2405.chmm the path needs it about once per sequence).
 template <int SM, int W, int HA, bool GE, bool STAMP = false, int DIAG = 0, int PATHS = 0>
-__global__ __launch_bounds__(64 * W, (GE && W == 4) ? 4 : 1) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
+__global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 : 1) void chain_viterbi_kernel(BandModel m, FusedBatch b) {
     static_assert(!PATHS || (HA == 1 && !GE && !STAMP && DIAG == 0), "decoded paths: HA 1, E in VGPRs");
     constexpr int HM = kBandHeavy;
     constexpr uint32_t B = 64 * W;
@@ -333,14 +333,23 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4) ? 4 : 1) void chain_viterbi_
     };
     // Arrivals the count of obs's slot has once every row published obs (obs >= first - 1).
     auto arrivals = [&](uint32_t obs) -> uint32_t { return (PUB1 ? 1u : 4u) * W * (((obs + 1u - first) / kRing) + 1u); };
-    // Bounded spins: `spins` is wave-uniform (every decision goes through readfirstlane).
-    uint32_t spins = 0, spins_b = 0;  // all slow-path re-reads / those of boundary words
+    // Bounded spins, per wait: one wait gives up after kSpinLimit re-reads (~0.1 s of s_sleep,
+    // never reached by a healthy run however long the sequence) and sets `gave_up`, after which
+    // no later wait of this wave spins (the results are void; the fault word reports it).
+    // `spins` / `spins_b` only count slow-path re-reads for the diagnostic stamps.  All of them
+    // are wave-uniform (every decision goes through readfirstlane).
+    uint32_t spins = 0, spins_b = 0;
+    bool gave_up = false;
     // min of the light scores of observation obs; (cnt, cell) hold a first read.
     auto take_mu = [&](uint32_t obs, uint32_t slot, uint32_t cnt, float cell) -> float {
         const uint32_t want = arrivals(obs);
         if (!NO_MU_WAIT && __builtin_expect((uint32_t)uniform((int)cnt) < want, 0)) {
             for (uint32_t k = 0;; ++k) {
-                if (++spins > kSpinLimit) break;
+                if (gave_up || k >= kSpinLimit) {
+                    gave_up = true;
+                    break;
+                }
+                ++spins;
                 if (k >= 2) __builtin_amdgcn_s_sleep(1);  // the first re-reads go straight out
                 cnt = __hip_atomic_load(pcnt + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 cell = __hip_atomic_load(pcell + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -356,9 +365,13 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4) ? 4 : 1) void chain_viterbi_
         uint64_t w = w0;
         if (!NO_BND_WAIT && __builtin_expect(uniform((int)(uint32_t)(w >> 32)) != (int)(obs + 1u), 0)) {
             const uint64_t* bp = rec_l + 2 * kMaxWaves * slot;
-            while (true) {
+            for (uint32_t k = 0;; ++k) {
+                if (gave_up || k >= kSpinLimit) {
+                    gave_up = true;
+                    break;
+                }
                 ++spins_b;
-                if (++spins > kSpinLimit) break;
+                ++spins;
                 __builtin_amdgcn_s_sleep(1);
                 w = lds_load64(bp);
                 if (uniform((int)(uint32_t)(w >> 32)) == (int)(obs + 1u)) break;
@@ -662,7 +675,7 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4) ? 4 : 1) void chain_viterbi_
         for (int k = 0; k < kBandStamps; ++k)
             m.stamps[((size_t)q * kMaxWaves + wave) * kBandStamps + k] = st_acc[k];
     }
-    if (spins > kSpinLimit && lane == 0 && m.fault) atomicOr(m.fault, 1u);
+    if (gave_up && lane == 0 && m.fault) atomicOr(m.fault, 1u);
 
     // ---- epilogue: scores and the lowest-index argmin ---------------------------------------
     float* out = b.scores + (size_t)q * n;

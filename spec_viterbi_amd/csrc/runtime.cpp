@@ -91,6 +91,17 @@ HostModel build_host_model(uint64_t n, uint64_t S, uint64_t nstart, const uint64
     if (ntrans >= (1ull << 32)) throw Error(SVH_E_UNSUPPORTED, "trans_num must be < 2^32");
     if (!emissions || (nstart && (!start_cols || !start_vals)) || (ntrans && (!src || !dst || !prob)))
         throw Error(SVH_E_INVALID, "null model array");
+    // Scores are -log2 p (HMM::to_modified_prob): finite or +inf.  A NaN or -inf (p = +inf)
+    // would let fl(-inf + +inf) = NaN into the min, whose result the kernels (built with
+    // -fno-honor-nans, so fminf is one v_min_f32) and GraphBLAS's GB_FMIN need not agree on.
+    // The reference's reader never produces either for p in [0, 1]; reject them here.
+    auto bad = [](float x) { return std::isnan(x) || x == -std::numeric_limits<float>::infinity(); };
+    for (uint64_t i = 0; i < nstart; ++i)
+        if (bad(start_vals[i])) throw Error(SVH_E_INVALID, "start score is NaN or -inf");
+    for (uint64_t i = 0; i < S * n; ++i)
+        if (bad(emissions[i])) throw Error(SVH_E_INVALID, "emission score is NaN or -inf");
+    for (uint64_t e = 0; e < ntrans; ++e)
+        if (bad(prob[e])) throw Error(SVH_E_INVALID, "transition score is NaN or -inf");
     HostModel h;
     h.n = (uint32_t)n;
     h.S = (uint32_t)S;
@@ -774,11 +785,12 @@ void Model::spec_build(uint32_t level, hipStream_t s) {
     spec_level = level;
 }
 
-svh_model_info Model::info() const {
+svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
     svh_model_info i;
     std::memset(&i, 0, sizeof(i));
-    const DevicePlan* p = plan_for(false);
-    const DeviceBandPlan* bpl = band_for(false);
+    const bool steps = level <= 1 || spec_level < 2;  // level >= 2 runs only the tail on step kernels
+    const DevicePlan* p = plan_for(paths && steps);
+    const DeviceBandPlan* bpl = band_for(paths && steps, nseq);
     i.kernel = bpl ? (bpl->plan.chain ? SVH_KERNEL_CHAIN : SVH_KERNEL_BAND) : p ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
     i.family = p ? p->plan.family : -1;
     i.threads = p ? (int32_t)p->plan.B : (int32_t)std::min<uint32_t>(1024, round_up(host.n, 64));
@@ -803,6 +815,8 @@ svh_model_info Model::info() const {
     i.spec_bytes = d_products.bytes;
     i.paths_kernel = band_for(true) ? SVH_KERNEL_CHAIN : plan_for(true) ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
     i.wide_threads = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.B : 0;
+    i.wide_slots = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.SM : 0;
+    i.cu_count = cu_count;
     return i;
 }
 
@@ -1266,7 +1280,11 @@ void Model::check_fault() const {
         if (!p->plan.ok || !p->view.fault) continue;
         uint32_t fault = 0;
         hip_check(hipMemcpy(&fault, p->view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
-        if (fault) throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
+        if (fault) {
+            // reported once: clear the word so the model's later runs are judged on their own
+            hip_check(hipMemset(p->view.fault, 0, 4), "fault reset");
+            throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
+        }
     }
 }
 

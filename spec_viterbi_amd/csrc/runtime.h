@@ -151,7 +151,7 @@ struct Model {
     // Chain plan to run for a pass over nseq sequences (nullptr: use plan_for(paths)).
     const DeviceBandPlan* band_for(bool paths, uint32_t nseq = 0) const;
     void spec_build(uint32_t level, hipStream_t s);
-    svh_model_info info() const;
+    svh_model_info info(uint32_t nseq = 0, bool paths = false, uint32_t level = 0) const;
     // throws if a chain-kernel bounded wait gave up since the model was created (synchronous)
     void check_fault() const;
     // one pass of the step kernel the model plans for (chain, band, fused or generic)

@@ -256,6 +256,13 @@ int svh_batch_elapsed_ms(svh_batch_t b, float* ms) {
     });
 }
 
+int svh_batch_plan(svh_batch_t b, uint32_t level, svh_model_info* info) {
+    return guarded([&] {
+        require(b && info, "null argument");
+        *info = b->impl->model->info(b->impl->nseq, b->impl->paths, level);
+    });
+}
+
 int svh_batch_destroy(svh_batch_t b) {
     return guarded([&] { delete b; });
 }

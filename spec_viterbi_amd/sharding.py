@@ -6,9 +6,10 @@ best final states and, optionally, decoded paths).  Assignment is LPT (longest p
 first, greedy onto the least-loaded rank) on sequence length, which bounds the makespan by the
 longest sequence plus one average share.
 
-The gathers are all_gather of padded fixed-width tensors: RCCL has no gather, and the payloads are
-tiny (covid-19.ess: 16 x 2407 fp32 scores + 15,616 path entries), so they are latency-bound on
-xGMI whatever the collective.  The same code runs over gloo on CPU tensors (the CPU tests).
+The gathers are `dist.gather` of padded fixed-width tensors to rank 0 (ncclGather-style: only
+rank 0 receives; the LPT assignment is deterministic, so no rank needs to exchange index lists).
+The payloads are tiny (covid-19.ess: 16 x 2407 fp32 scores + 15,616 path entries), so they are
+latency-bound on xGMI.  The same code runs over gloo on CPU tensors (the CPU tests).
 """
 from __future__ import annotations
 
@@ -36,51 +37,58 @@ def lpt_assign(lengths, world_size: int) -> list[list[int]]:
     return out
 
 
-def _gather_rows(local_idx, rows: np.ndarray, nseq: int, fill, group=None, device=None):
-    """All-gather per-rank rows [len(local_idx), width] and place them by global index on rank 0.
+def _gather_rows(assignment, rows: np.ndarray, nseq: int, fill, group=None, device=None):
+    """Gather per-rank rows [len(assignment[rank]), width] to rank 0, placed by global index.
 
-    Every rank pads its rows to the largest local count; one all_gather of the padded tensor plus
-    one of the index lists.  Returns [nseq, width] on rank 0, None elsewhere.
+    `assignment` is the full LPT assignment (deterministic, so every rank holds it): each rank
+    pads its rows to the largest share and one `dist.gather` (RCCL gather on GPUs, gloo on
+    CPUs) brings them to rank 0, which alone allocates the receive buffers.  Returns
+    [nseq, width] on rank 0, None elsewhere.
     """
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    mine = assignment[rank]
     rows = np.asarray(rows)
     width = rows.shape[1] if rows.ndim == 2 else 1
-    counts = [None] * world
-    dist.all_gather_object(counts, (len(local_idx), list(map(int, local_idx))), group=group)
-    height = max(max(c for c, _ in counts), 1)
+    height = max(max(len(a) for a in assignment), 1)
     dtype = torch.from_numpy(np.zeros(0, rows.dtype)).dtype
     buf = torch.full((height, width), fill, dtype=dtype, device=device)
-    if len(local_idx):
-        buf[: len(local_idx)] = torch.from_numpy(np.ascontiguousarray(rows.reshape(len(local_idx), width))).to(buf.device)
-    gathered = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(gathered, buf, group=group)
+    if len(mine):
+        buf[: len(mine)] = torch.from_numpy(np.ascontiguousarray(rows.reshape(len(mine), width))).to(buf.device)
+    recv = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, recv, dst=0, group=group)
     if rank != 0:
         return None
     out = np.full((nseq, width), fill, rows.dtype)
     for r in range(world):
-        got = gathered[r].cpu().numpy()
-        for k, q in enumerate(counts[r][1]):
+        got = recv[r].cpu().numpy()
+        for k, q in enumerate(assignment[r]):
             out[q] = got[k]
     return out
 
 
-def gather_scores(local_idx, local_scores: np.ndarray, nseq: int, n: int, group=None, device=None):
-    """Per-rank score rows [len(local_idx), n] -> [nseq, n] fp32 on rank 0 (None elsewhere)."""
-    rows = np.asarray(local_scores, np.float32).reshape(len(local_idx), n)
-    return _gather_rows(local_idx, rows, nseq, float("inf"), group, device)
+def gather_scores(assignment, local_scores: np.ndarray, nseq: int, n: int, group=None, device=None):
+    """Per-rank score rows [len(assignment[rank]), n] -> [nseq, n] fp32 on rank 0 (None elsewhere)."""
+    import torch.distributed as dist
+
+    mine = assignment[dist.get_rank(group)]
+    rows = np.asarray(local_scores, np.float32).reshape(len(mine), n)
+    return _gather_rows(assignment, rows, nseq, float("inf"), group, device)
 
 
-def gather_paths(local_idx, local_paths, lengths, group=None, device=None):
+def gather_paths(assignment, local_paths, lengths, group=None, device=None):
     """Per-rank decoded paths (int32 arrays) -> list of nseq paths on rank 0 (None elsewhere)."""
+    import torch.distributed as dist
+
+    mine = assignment[dist.get_rank(group)]
     width = max([int(x) for x in lengths] + [1])
-    rows = np.full((len(local_idx), width), -1, np.int32)
+    rows = np.full((len(mine), width), -1, np.int32)
     for k, p in enumerate(local_paths):
         rows[k, : len(p)] = p
-    out = _gather_rows(local_idx, rows, len(lengths), -1, group, device)
+    out = _gather_rows(assignment, rows, len(lengths), -1, group, device)
     if out is None:
         return None
     return [out[q, : int(lengths[q])].copy() for q in range(len(lengths))]
@@ -131,7 +139,8 @@ def run_sharded(hmm, seqs, *, level: int = 0, paths: bool = False, group=None, d
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     lengths = [int(np.asarray(s).size) for s in seqs]
-    mine = lpt_assign(lengths, world)[rank]
+    assignment = lpt_assign(lengths, world)
+    mine = assignment[rank]
     if compute is None:
         index = torch.device(device).index if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
         compute = _hip_compute(index or 0, time_parallel)
@@ -150,9 +159,9 @@ def run_sharded(hmm, seqs, *, level: int = 0, paths: bool = False, group=None, d
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     seconds = float(t.item())
-    all_scores = gather_scores(mine, scores, len(seqs), n, group, device)
-    all_best = _gather_rows(mine, np.asarray(best, np.int64).reshape(-1, 1), len(seqs), -1, group, device)
-    all_paths = gather_paths(mine, local_paths, lengths, group, device) if paths else None
+    all_scores = gather_scores(assignment, scores, len(seqs), n, group, device)
+    all_best = _gather_rows(assignment, np.asarray(best, np.int64).reshape(-1, 1), len(seqs), -1, group, device)
+    all_paths = gather_paths(assignment, local_paths, lengths, group, device) if paths else None
     if rank != 0:
         return None, None, None, seconds
     return all_scores, all_best.reshape(-1), all_paths, seconds

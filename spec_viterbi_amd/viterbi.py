@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import abc
 import ctypes
+import hashlib
 
 import numpy as np
 
@@ -127,6 +128,13 @@ class DeviceBatch:
         _lib.check(_lib.lib.svh_batch_device_results(self._h, ctypes.byref(s), ctypes.byref(b)))
         return int(s.value or 0), int(b.value or 0)
 
+    def plan(self, level: int = 0) -> dict:
+        """The plan run(level) launches for this batch (svh_batch_plan): model info fields with
+        kernel / threads / slots of the narrow or wide chain plan this batch selects."""
+        i = _lib.svh_model_info()
+        _lib.check(_lib.lib.svh_batch_plan(self._h, int(level), ctypes.byref(i)))
+        return {name: getattr(i, name) for name, _ in i._fields_}
+
     def elapsed_ms(self) -> float:
         ms = ctypes.c_float()
         _lib.check(_lib.lib.svh_batch_elapsed_ms(self._h, ctypes.byref(ms)))
@@ -170,17 +178,36 @@ class Viterbi_spec_impl(abc.ABC):
         return self.level
 
 
+def hmm_fingerprint(hmm: HMM) -> bytes:
+    """Content digest of an HMM (every field the device model is built from), the Python
+    counterpart of HIP_impl.cpp's fingerprint: equal digests <=> the same device model."""
+    h = hashlib.blake2b(digest_size=16)
+    h.update(np.array([hmm.states_num, hmm.emit_num], np.uint64).tobytes())
+    for a in (hmm.trans_rows, hmm.trans_cols, hmm.trans_probs, hmm.emissions, hmm.start_probabilities_cols,
+              hmm.start_probabilities):
+        a = np.ascontiguousarray(a)
+        h.update(np.array([a.size], np.uint64).tobytes())
+        h.update(a.tobytes())
+    return h.digest()
+
+
 class HIP_impl(Viterbi_impl):
-    """MI355X backend of Viterbi_impl; the device model is cached per HMM object."""
+    """MI355X backend of Viterbi_impl.  The device model is cached by the HMM's content
+    fingerprint (not its identity: a freed HMM's id can be reused, and an HMM can be changed in
+    place), so every call runs the HMM it was given, as GraphBLAS_impl::run_Viterbi does
+    (GraphBLAS_impl.cpp:9-54 builds the model from its argument on every call)."""
 
     def __init__(self, device: int = -1, **model_opts):
         self.device = device
         self.model_opts = model_opts
-        self._cache: tuple[int, DeviceModel] | None = None
+        self._cache: tuple[bytes, DeviceModel] | None = None
 
     def _model(self, hmm: HMM) -> DeviceModel:
-        if self._cache is None or self._cache[0] != id(hmm):
-            self._cache = (id(hmm), DeviceModel(hmm, self.device, **self.model_opts))
+        key = hmm_fingerprint(hmm)
+        if self._cache is None or self._cache[0] != key:
+            if self._cache is not None:
+                self._cache[1].close()
+            self._cache = (key, DeviceModel(hmm, self.device, **self.model_opts))
         return self._cache[1]
 
     def run_Viterbi(self, hmm: HMM, seq) -> np.ndarray:

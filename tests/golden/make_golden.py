@@ -53,7 +53,7 @@ def main():
         "test_chmms": [case(f"chmm_files/test_chmms/{i}_test_chmm.chmm", f"ess_files/test_sequences/{i}_test_seq.ess",
                             range(2 if i == 0 else 1), levels=(1, 2, 3)) for i in range(4)],
         "chmm100_emit3": case("chmm_files/100.chmm", "ess_files/emit_3_3500_20.ess", range(3), levels=(2,)),
-        "chmm2405_emit50": case("chmm_files/2405.chmm", "ess_files/emit_50_3500_20.ess", range(2)),
+        "chmm2405_emit50": case("chmm_files/2405.chmm", "ess_files/emit_50_3500_20.ess", range(2), levels=(2,)),
     }
     for name, val in goldens.items():
         with open(os.path.join(OUT, f"{name}.json"), "w") as f:

@@ -347,3 +347,68 @@ def test_wide_batch_streamed_plan_2405():
         ref = oracle.viterbi(hmm, seqs[q])
         assert bit_equal(wide[q], ref), (q, first_mismatch(wide[q], ref))
         assert wide_best[q] == int(np.argmin(ref)), q
+
+
+def test_chain_long_sequence_no_fault():
+    """A 10 M-observation sequence on 8 waves of the chain kernel (the most inter-wave waits per
+    observation): every bounded wait is per wait, so length alone never trips the fault word
+    (round-1 budget was cumulative per sequence).  Scores bit-exact against the oracle."""
+    hmm = svh.read_HMM(chmm("100.chmm"))
+    rng = np.random.default_rng(7)
+    seq = rng.integers(0, hmm.emit_num, size=10_000_000).astype(np.uint64)
+    os.environ["SVH_CHAIN_WAVES"] = "8"
+    try:
+        model = svh.DeviceModel(hmm)
+    finally:
+        os.environ.pop("SVH_CHAIN_WAVES", None)
+    info = model.info()
+    assert info["kernel"] == _lib.SVH_KERNEL_CHAIN and info["threads"] == 512, info
+    got, best = model.viterbi([seq])
+    ref = oracle.viterbi(hmm, seq)
+    assert bit_equal(got[0], ref), first_mismatch(got[0], ref)
+    # and the model stays usable (no stale fault) on a second run
+    got2, _ = model.viterbi([seq[:5000]])
+    assert bit_equal(got2[0], oracle.viterbi(hmm, seq[:5000]))
+
+
+def test_hip_impl_cache_follows_the_hmm_passed():
+    """HIP_impl must always use the HMM passed in (reference semantics), even when a temporary
+    HMM is freed and the next one reuses its address, or an HMM is modified in place."""
+    impl = svh.HIP_impl()
+    seq = svh.read_emit_seq(ess("emit_3_3500_20.ess"))[0][:300]
+    for name in ("100.chmm", "200.chmm", "100.chmm", "300.chmm"):
+        got = impl.run_Viterbi(svh.read_HMM(chmm(name)), seq)  # temporary HMM each time
+        assert bit_equal(got, oracle.viterbi(svh.read_HMM(chmm(name)), seq)), name
+    hmm = svh.read_HMM(chmm("100.chmm"))
+    a = impl.run_Viterbi(hmm, seq)
+    hmm.trans_probs = hmm.trans_probs + np.float32(0.5)  # in-place change of the same object
+    b = impl.run_Viterbi(hmm, seq)
+    assert bit_equal(b, oracle.viterbi(hmm, seq)) and not bit_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["1301.chmm", "1509.chmm", "1901.chmm", "2365.chmm"])
+def test_wide_plan_other_pfam_models(name):
+    """The wide chain plan (picked for batches of more sequences than CUs) on other eligible Pfam
+    models: every sequence equal to narrow batches of the same sequences, a sample bit-exact
+    against the oracle; svh_batch_plan names the plan each batch runs."""
+    hmm = svh.read_HMM(chmm(name))
+    model = svh.DeviceModel(hmm)
+    info = model.info()
+    if not info["wide_threads"]:
+        pytest.skip(f"{name}: no wide plan ({info['threads']} threads narrow)")
+    rng = np.random.default_rng(5)
+    lens = [1, 8, 9, 17] + list(rng.integers(1, 200, size=info["cu_count"] + 40))
+    seqs = [rng.integers(0, hmm.emit_num, size=int(k)).astype(np.uint64) for k in lens]
+    batch = model.batch(seqs)
+    plan = batch.plan()
+    assert plan["threads"] == info["wide_threads"] and plan["slots"] == info["wide_slots"], plan
+    batch.run()
+    wide, wide_best = batch.read()
+    small = model.batch(seqs[:100])
+    assert small.plan()["threads"] == info["threads"]
+    narrow = np.concatenate([model.viterbi(seqs[k:k + 100])[0] for k in range(0, len(seqs), 100)])
+    assert bit_equal(wide, narrow)
+    for q in [0, 1, 2, 3, 150, len(seqs) - 1]:
+        ref = oracle.viterbi(hmm, seqs[q])
+        assert bit_equal(wide[q], ref), (q, first_mismatch(wide[q], ref))
+        assert wide_best[q] == int(np.argmin(ref)), q

@@ -58,3 +58,24 @@ def test_spec_level2_500_model():
         assert bit_equal(got[q], ref), (q, first_mismatch(got[q], ref))
         # and within the reference's tolerance of the non-spec answer
         assert all(svh.almost_equal(a, b) for a, b in zip(got[q], oracle.viterbi(hmm, seq)))
+
+
+def test_spec_level2_2405_emit50_config4():
+    """BASELINE config 4: 2405.chmm x emit_50_3500_20.ess on the _spec level-2 path (400 dense
+    2407 x 2408 products, 9.3 GB of HBM; reference GraphBLAS_spec_impl.cpp:15-36, :68-80).
+    All 50 sequences run in one batch; sequences 0..1 are compared bit-exact against the oracle's
+    committed level-2 vectors, every sequence against the non-spec goldens' tolerance rule
+    (HMM::almost_equal, |diff| <= 1, the reference's own semantic-equality bound)."""
+    g = load_golden("chmm2405_emit50")
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
+    impl = svh.HIP_spec_impl(2)
+    impl.spec_with(hmm)
+    got = impl.run_Viterbi_spec_batch(seqs)
+    assert got.shape == (50, hmm.states_num)
+    for rec in g["sequences"]:
+        ref = from_hex(rec["spec"]["2"])
+        assert bit_equal(got[rec["index"]], ref), (rec["index"], first_mismatch(got[rec["index"]], ref))
+    nonspec = svh.DeviceModel(hmm).viterbi(seqs)[0]
+    assert np.all(np.abs(got - nonspec) <= 1.0)
+    assert not np.array_equal(got, nonspec)  # level 2 really took the product path

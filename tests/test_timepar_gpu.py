@@ -126,3 +126,24 @@ def test_sharded_runner_time_parallel():
             run_sharded(hmm, seqs[:2], paths=True, time_parallel=(1024, 128))
         finally:
             dist.destroy_process_group()
+
+
+def test_time_parallel_rows_beyond_cu_count_run_the_wide_plan():
+    """Short segments give more launch rows (segments x basis runs) than CUs, so the step
+    launches of the time-parallel pass take the wide chain plan, with rows that start from
+    v_in at observations > 0: forced re-runs must be bit-exact, converged runs within tolerance."""
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("covid-19.ess"))
+    model = svh.DeviceModel(hmm)
+    assert model.info()["wide_threads"], model.info()
+    assert sum(len(s) for s in seqs) // 64 * 3 > model.info()["cu_count"]
+    one_s, one_b = model.viterbi(seqs)
+    batch = model.batch(seqs)
+    fb = batch.run_time_parallel(seg_len=64, probe_len=32, rel_tol=-1.0)
+    assert fb > model.info()["cu_count"] // 3
+    scores, best = batch.read()
+    assert bit_equal(scores, one_s) and np.array_equal(best, one_b)
+    batch.run_time_parallel(seg_len=128, probe_len=64)
+    scores, best = batch.read()
+    for q in range(len(seqs)):
+        assert close(scores[q], one_s[q]), q
