@@ -11,6 +11,10 @@ from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_uint32
 
 LIB_NAME = "libspec_viterbi_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# A/B timing of alternative builds of the same engine (tools/ab_lib.sh): another in-tree build of
+# this library, never a fallback (it must exist, or import fails as for the default).
+if os.environ.get("SVH_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["SVH_LIB"])
 
 SVH_OK = 0
 SVH_E_INVALID = -1

@@ -333,23 +333,21 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
     };
     // Arrivals the count of obs's slot has once every row published obs (obs >= first - 1).
     auto arrivals = [&](uint32_t obs) -> uint32_t { return (PUB1 ? 1u : 4u) * W * (((obs + 1u - first) / kRing) + 1u); };
-    // Bounded spins, per wait: one wait gives up after kSpinLimit re-reads (~0.1 s of s_sleep,
-    // never reached by a healthy run however long the sequence) and sets `gave_up`, after which
-    // no later wait of this wave spins (the results are void; the fault word reports it).
-    // `spins` / `spins_b` only count slow-path re-reads for the diagnostic stamps.  All of them
-    // are wave-uniform (every decision goes through readfirstlane).
-    uint32_t spins = 0, spins_b = 0;
-    bool gave_up = false;
+    // Bounded spins.  `spins` counts slow-path re-reads against kSpinLimit (~0.1 s of s_sleep);
+    // past it every wait gives up at once (a broken launch drains) and the epilogue sets the
+    // fault word (SVH_E_HIP on the host).  The budget is per symbol chunk, not per sequence: the
+    // refill below (every kChainSymChunk = 32768 observations) resets a healthy counter, so a
+    // healthy run (well under one re-read per observation) never trips it however long the
+    // sequence, while a stuck wait still gives up within one budget.  The reset lives in the
+    // refill branch only: per-wait counters or a give-up flag in the wait loops changed the
+    // compiler's code for the hot waits and cost 2-14%.  Wave-uniform throughout.
+    uint32_t spins = 0, spins_b = 0;  // all slow-path re-reads / those of boundary words
     // min of the light scores of observation obs; (cnt, cell) hold a first read.
     auto take_mu = [&](uint32_t obs, uint32_t slot, uint32_t cnt, float cell) -> float {
         const uint32_t want = arrivals(obs);
         if (!NO_MU_WAIT && __builtin_expect((uint32_t)uniform((int)cnt) < want, 0)) {
             for (uint32_t k = 0;; ++k) {
-                if (gave_up || k >= kSpinLimit) {
-                    gave_up = true;
-                    break;
-                }
-                ++spins;
+                if (++spins > kSpinLimit) break;
                 if (k >= 2) __builtin_amdgcn_s_sleep(1);  // the first re-reads go straight out
                 cnt = __hip_atomic_load(pcnt + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 cell = __hip_atomic_load(pcell + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -365,13 +363,9 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
         uint64_t w = w0;
         if (!NO_BND_WAIT && __builtin_expect(uniform((int)(uint32_t)(w >> 32)) != (int)(obs + 1u), 0)) {
             const uint64_t* bp = rec_l + 2 * kMaxWaves * slot;
-            for (uint32_t k = 0;; ++k) {
-                if (gave_up || k >= kSpinLimit) {
-                    gave_up = true;
-                    break;
-                }
+            while (true) {
                 ++spins_b;
-                ++spins;
+                if (++spins > kSpinLimit) break;
                 __builtin_amdgcn_s_sleep(1);
                 w = lds_load64(bp);
                 if (uniform((int)(uint32_t)(w >> 32)) == (int)(obs + 1u)) break;
@@ -603,6 +597,7 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
         for (; i + kRing <= len; i = (uint32_t)uniform((int)(i + kRing))) {
             if (__builtin_expect(i + 2 * kRing > sbase + kChainSymChunk, 0)) {  // uniform: refill (rare)
                 __syncthreads();  // every wave is at observation i: the old chunk is dead
+                spins = spins > kSpinLimit ? spins : 0u;  // new chunk, new budget (a give-up sticks)
                 sbase = i & ~15u;
                 stage_symbols();
                 __syncthreads();
@@ -675,7 +670,7 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
         for (int k = 0; k < kBandStamps; ++k)
             m.stamps[((size_t)q * kMaxWaves + wave) * kBandStamps + k] = st_acc[k];
     }
-    if (gave_up && lane == 0 && m.fault) atomicOr(m.fault, 1u);
+    if (spins > kSpinLimit && lane == 0 && m.fault) atomicOr(m.fault, 1u);
 
     // ---- epilogue: scores and the lowest-index argmin ---------------------------------------
     float* out = b.scores + (size_t)q * n;
