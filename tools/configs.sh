@@ -12,7 +12,8 @@ $B --steps 20 > "$OUT/c3_2405_emit50.json" 2> "$OUT/c3.err" &&
 $B --steps 10 --paths > "$OUT/c3_2405_emit50_paths.json" 2> "$OUT/c3p.err" &&
 $B --steps 20 --level 1 > "$OUT/c4_2405_emit50_spec1.json" 2> "$OUT/c4a.err" &&
 $B --steps 3 --warmup 1 --level 2 > "$OUT/c4_2405_emit50_spec2.json" 2> "$OUT/c4b.err" &&
-$B --steps 20 --ess covid-19.ess > "$OUT/c5_2405_covid_1gpu.json" 2> "$OUT/c5.err" &&
+$B --steps 20 --shard covid > "$OUT/c5_2405_covid_1gpu.json" 2> "$OUT/c5.err" &&
+$B --steps 5 --warmup 2 --replicate 160 > "$OUT/c3_2405_emit50_x160_wide.json" 2> "$OUT/c3w.err" &&
 timeout -k 10 300 python -m spec_viterbi_amd.run_sharded --model data/chmm_files/2405.chmm \
     --ess data/ess_files/covid-19.ess --paths > "$OUT/c5_sharded_1rank_paths.json" 2> "$OUT/c5s.err"
 rc=$?
