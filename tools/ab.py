@@ -38,7 +38,11 @@ def main():
         model = svh.DeviceModel(hmm, kernel=int(kv.get("kernel", "0")), max_threads=int(kv.get("threads", "0")))
         batch = model.batch(seqs)
         batch.run()
-        scores, _ = batch.read()
+        try:
+            scores, _ = batch.read()
+        except svh.viterbi._lib.SvhError as e:  # diagnostic ablations that break the exchange
+            print(f"{spec}: {e}", flush=True)   # (DIAG 2/4) trip the bounded waits by design
+            scores = np.full((len(seqs), hmm.states_num), np.nan, np.float32)
         if ref is None:
             ref = scores
         same = bool(np.all((scores.view(np.uint32) == ref.view(np.uint32)) | ((scores == 0) & (ref == 0))))
@@ -47,6 +51,10 @@ def main():
         for spec, model, batch, times, _, _ in variants:
             batch.run()
             times.append(batch.elapsed_ms())
+            try:
+                batch.read()
+            except svh.viterbi._lib.SvhError:
+                pass
     for spec, model, batch, times, same, info in variants:
         med = statistics.median(times)
         print(f"{spec:24s} kernel={info['kernel']} B={info['threads']} SM={info['slots']} "
