@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kMaxBandThreads) void band_viterbi_kernel(BandModel
         for (int h = 0; h < HM; ++h) {
             float a = cst[kBandTailA + h] + mu;
 #pragma unroll
-            for (int k = 0; k < HM; ++k) a = fminf(a, cst[kBandTailX + h * HM + k] + vh[k]);
+            for (int k = 0; k < HM; ++k) a = fminf(a, cst[band_tail_x(h, k)] + vh[k]);
             vhn[h] = a;
         }
 

@@ -33,6 +33,7 @@ using namespace dev;
 namespace {
 
 typedef float f32x32 __attribute__((ext_vector_type(32)));
+typedef float f2 __attribute__((ext_vector_type(2)));  // one v_pk_*_f32 operand (aligned VGPR pair)
 
 constexpr uint32_t kRing = kChainRing;  // see the ring argument at the exchange
 constexpr uint32_t kSpinLimit = 1u << 22;
@@ -234,13 +235,26 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
             pin(e);  // all SM extractions adjacent: one s_set_gpr_idx_on .. off block
         }
     };
-    float aw[HA][SM], bw[SM];
+    // Packed fp32: slots (2k, 2k+1) are computed as pairs with v_pk_add_f32 (IEEE adds, bit-identical
+    // to two v_add_f32), an odd last slot alone.  The light scores live in pairs
+    // P[k] = (slot 2k-1, slot 2k), slot -1 being the chain input p0 of slot 0, so the chain operand
+    // of the pair (2k, 2k+1) -- slots (2k-1, 2k) -- is the register pair P[k] itself.
+    constexpr int NK = SM / 2, NP = SM / 2 + 1;
+    f2 BW2[NK > 0 ? NK : 1], AW2[HA][NK > 0 ? NK : 1];
+    float bwS = 0.0f, awS[HA];
 #pragma unroll
-    for (int s = 0; s < SM; ++s) {
-        bw[s] = m.bw[s * B + t];
+    for (int k = 0; k < NK; ++k) {
+        BW2[k] = (f2){m.bw[2 * k * B + t], m.bw[(2 * k + 1) * B + t]};
 #pragma unroll
-        for (int h = 0; h < HA; ++h) aw[h][s] = m.aw[(size_t)h * tail + s * B + t];
+        for (int h = 0; h < HA; ++h)
+            AW2[h][k] = (f2){m.aw[(size_t)h * tail + 2 * k * B + t], m.aw[(size_t)h * tail + (2 * k + 1) * B + t]};
     }
+    if constexpr (SM & 1) {
+        bwS = m.bw[(SM - 1) * B + t];
+#pragma unroll
+        for (int h = 0; h < HA; ++h) awS[h] = m.aw[(size_t)h * tail + (SM - 1) * B + t];
+    }
+
     for (uint32_t x = t; x < S * kBandTail; x += B)
         ctab[x] = m.erows[(size_t)(x / kBandTail) * erow + tail + x % kBandTail];
     for (uint32_t x = t; x < 2 * kRing * kMaxWaves; x += B) rec[x] = 0ull;  // tag 0: never written
@@ -263,13 +277,23 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
     };
     stage_symbols();
     __syncthreads();  // symbols, constants and tags initialised: the only barrier before the epilogue
-    float v[SM], vh[HM];
+    f2 P[NP];  // light scores: P[k] = (slot 2k-1, slot 2k) (see the packed-fp32 note above)
+    auto vg = [&](int s) -> float { return P[(s + 1) >> 1][(s + 1) & 1]; };
+    auto vs = [&](int s, float x) { P[(s + 1) >> 1][(s + 1) & 1] = x; };
+    auto vcopy = [&](float (&o)[SM]) {
+#pragma unroll
+        for (int s = 0; s < SM; ++s) o[s] = vg(s);
+    };
+    vs(-1, kInf);
+    if constexpr (!(SM & 1)) P[NP - 1][1] = kInf;  // unused high half of the last pair
+    f2 vh;  // heavy scores (N, C) as one pair: the packed heavy update below and the light rows'
+            // broadcast operand (op_sel) read it as a whole
     if (first == 0) {
         const uint32_t o0 = (uint32_t)uniform((int)symr[0]);
         float e0[SM];
         extract(o0, e0);
 #pragma unroll
-        for (int s = 0; s < SM; ++s) v[s] = e0[s] + m.start[s * B + t];  // diag(E[s0]) (x) start
+        for (int s = 0; s < SM; ++s) vs(s, e0[s] + m.start[s * B + t]);  // diag(E[s0]) (x) start
 #pragma unroll
         for (int h = 0; h < HM; ++h)
             vh[h] = m.hvalid[h] ? ctab[o0 * kBandTail + kBandTailE + h] + m.hstart[h] : kInf;
@@ -279,7 +303,7 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
 #pragma unroll
         for (int s = 0; s < SM; ++s) {
             const uint32_t r = m.lrow[s * B + t];
-            v[s] = r != 0xFFFFFFFFu ? vin[r] : kInf;
+            vs(s, r != 0xFFFFFFFFu ? vin[r] : kInf);
         }
 #pragma unroll
         for (int h = 0; h < HM; ++h) vh[h] = m.hvalid[h] ? vin[m.hrow[h]] : kInf;
@@ -382,19 +406,14 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
         return {*reinterpret_cast<const float4*>(ctab + o * kBandTail),
                 *reinterpret_cast<const float2*>(ctab + o * kBandTail + 4)};
     };
-    // heavy scores from mu (partials) and their previous values
+    // heavy scores from mu (partials) and their previous values, both rows at once:
+    //   vh'[h] = min(fl(A_h + mu), fl(X_hh + vh[h]), fl(X_hk + vh[k]))   (tail: band_tail_x)
+    static_assert(kBandTailA == 0 && band_tail_x(0, 0) == 2 && band_tail_x(0, 1) == 4, "tail layout");
     auto heavy_update = [&](float mu, const HeavyConst& hc) {
-        const float cst[6] = {hc.c0.x, hc.c0.y, hc.c0.z, hc.c0.w, hc.c1.x, hc.c1.y};
-        float vhn[HM];
-#pragma unroll
-        for (int h = 0; h < HM; ++h) {
-            float a = cst[kBandTailA + h] + mu;
-#pragma unroll
-            for (int k = 0; k < HM; ++k) a = fminf(a, cst[kBandTailX + h * HM + k] + vh[k]);
-            vhn[h] = a;
-        }
-#pragma unroll
-        for (int h = 0; h < HM; ++h) vh[h] = vhn[h];
+        const f2 a = (f2){hc.c0.x, hc.c0.y} + (f2){mu, mu};
+        const f2 d = (f2){hc.c0.z, hc.c0.w} + vh;
+        const f2 x = (f2){hc.c1.x, hc.c1.y} + vh.yx;
+        vh = (f2){fminf(fminf(a.x, d.x), x.x), fminf(fminf(a.y, d.y), x.y)};
     };
 
     // ---- decoded paths ------------------------------------------------------------------------
@@ -426,7 +445,9 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
             const bool ec = f & 1u, ea = f & 2u, hl = f & 4u;
             pmC[s] = __builtin_amdgcn_ballot_w64(ea && (!ec || hl));
         }
-        checkpoint(0, v);  // v_0
+        float v0[SM];
+        vcopy(v0);
+        checkpoint(0, v0);  // v_0
     }
     // Heavy-row record of observation obs (record row obs-1): the inputs of its backpointers --
     // the heavy scores vo of obs-1 and the light minimum mu of obs-1 -- stored by wave 0; the
@@ -465,18 +486,31 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
         uint64_t bwv = 0;
         if constexpr (W > 1) bwv = lds_load64(rec_l + 2 * kMaxWaves * s1);
         const HeavyConst hc = load_heavy(o);
-        // terms that do not need the heavy scores (lane 0's slot 0 is redone below)
-        const float p0 = wave_shr1(v[SM - 1], kInf);
-        float xb[SM], xa[HA][SM];
+        // terms that do not need the heavy scores (lane 0's slot 0 is redone below):
+        // xb = fl(fl(E + bw) + v_prev), xa = fl(E + aw), in pairs
+        vs(-1, wave_shr1(vg(SM - 1), kInf));  // p0
+        f2 eb2[NK > 0 ? NK : 1], xb2[NK > 0 ? NK : 1], xa2[HA][NK > 0 ? NK : 1];
+        float ebS = 0.0f, xbS = 0.0f, xaS[HA];
 #pragma unroll
-        for (int s = 0; s < SM; ++s) {
-            xb[s] = (e[s] + bw[s]) + (s == 0 ? p0 : v[s - 1]);
+        for (int k = 0; k < NK; ++k) {
+            const f2 e2 = {e[2 * k], e[2 * k + 1]};
+            eb2[k] = e2 + BW2[k];
+            xb2[k] = eb2[k] + P[k];
 #pragma unroll
-            for (int h = 0; h < HA; ++h) xa[h][s] = e[s] + aw[h][s];
+            for (int h = 0; h < HA; ++h) xa2[h][k] = e2 + AW2[h][k];
         }
+        if constexpr (SM & 1) {
+            ebS = e[SM - 1] + bwS;
+            xbS = ebS + vg(SM - 2);
+#pragma unroll
+            for (int h = 0; h < HA; ++h) xaS[h] = e[SM - 1] + awS[h];
+        }
+        auto xbv = [&](int s) -> float { return (SM & 1) && s == SM - 1 ? xbS : xb2[s >> 1][s & 1]; };
+        auto xav = [&](int h, int s) -> float { return (SM & 1) && s == SM - 1 ? xaS[h] : xa2[h][s >> 1][s & 1]; };
         // the exchange reads were issued first; everything above ran while they were in flight
-        pin(xb);
-        pin(xa[0]);
+#pragma unroll
+        for (int k = 0; k < NK; ++k) asm volatile("" : "+v"(xb2[k]), "+v"(xa2[0][k]));
+        if constexpr (SM & 1) asm volatile("" : "+v"(xbS), "+v"(xaS[0]));
         if constexpr (W > 1) {
             if (lagged) asm volatile("" : "+v"(pmv), "+v"(pcv));
         }
@@ -498,11 +532,21 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
         mark(2);
         float vn[SM];
 #pragma unroll
-        for (int s = 0; s < SM; ++s) {
-            float r = xb[s];
+        for (int k = 0; k < NK; ++k) {
+            f2 r = xb2[k];
 #pragma unroll
-            for (int h = 0; h < HA; ++h) r = fminf(r, xa[h][s] + vh[h]);
-            vn[s] = r;
+            for (int h = 0; h < HA; ++h) {
+                const f2 x = xa2[h][k] + (f2){vh[h], vh[h]};
+                r = (f2){fminf(r.x, x.x), fminf(r.y, x.y)};
+            }
+            vn[2 * k] = r.x;
+            vn[2 * k + 1] = r.y;
+        }
+        if constexpr (SM & 1) {
+            float r = xbS;
+#pragma unroll
+            for (int h = 0; h < HA; ++h) r = fminf(r, xaS[h] + vh[h]);
+            vn[SM - 1] = r;
         }
         mark(3);
         pin(vn);  // the light scores first: the boundary word has had the most time to land
@@ -510,17 +554,17 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
         float xb0 = 0.0f;
         {
             const float bv = take_bnd(i - 1, s1, bwv);
-            float r = (e[0] + bw[0]) + bv;
-            if constexpr (PATHS) xb0 = lane == 0 ? r : xb[0];
+            float r = (NK > 0 ? eb2[0].x : ebS) + bv;
+            if constexpr (PATHS) xb0 = lane == 0 ? r : xbv(0);
 #pragma unroll
-            for (int h = 0; h < HA; ++h) r = fminf(r, xa[h][0] + vh[h]);
+            for (int h = 0; h < HA; ++h) r = fminf(r, xav(h, 0) + vh[h]);
             vn[0] = lane == 0 ? r : vn[0];
         }
         if constexpr (PATHS) {  // light masks of observation i (record row i-1)
             auto mask_slot = [&](auto sc) {
                 constexpr int s = decltype(sc)::value;
-                const float xh = xa[0][s] + vh[0];
-                const float xbe = s == 0 ? xb0 : xb[s];
+                const float xh = xav(0, s) + vh[0];
+                const float xbe = s == 0 ? xb0 : xbv(s);
                 // heavy term taken: below the chain term, or tied and winning the tie
                 if constexpr (PATHS == 2)
                     push_le(macc[s], xh, xbe);
@@ -545,7 +589,7 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
             }
         }
 #pragma unroll
-        for (int s = 0; s < SM; ++s) v[s] = vn[s];
+        for (int s = 0; s < SM; ++s) vs(s, vn[s]);
         return hc;
     };
 
@@ -566,10 +610,14 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
         return with_slot(i, [&](auto kc) { return step(i, kc, lagged, o, e, hcp); });
     };
     if constexpr (W > 1) {
-        const float rm = row_partial(v);
-        with_slot(first - 1, [&](auto kc) { publish(kc, first - 1, rm, v[SM - 1]); });
+        float v0[SM];
+        vcopy(v0);
+        const float rm = row_partial(v0);
+        with_slot(first - 1, [&](auto kc) { publish(kc, first - 1, rm, v0[SM - 1]); });
     } else {
-        own_p1 = uniform_f(wave_partial(v));
+        float v0[SM];
+        vcopy(v0);
+        own_p1 = uniform_f(wave_partial(v0));
     }
     auto sym_dword = [&](uint32_t i) -> uint64_t {  // symbols i .. i+7 (i % 8 == 0)
         return *reinterpret_cast<const uint64_t*>(symr + (i - sbase));
@@ -680,8 +728,8 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
     for (int s = 0; s < SM; ++s) {
         const uint32_t r = m.lrow[s * B + t];
         if (r != 0xFFFFFFFFu) {
-            out[r] = v[s];
-            lex_min(bvv, bk, v[s], r);
+            out[r] = vg(s);
+            lex_min(bvv, bk, vg(s), r);
         }
     }
     if (t < (uint32_t)HM && m.hvalid[t]) out[m.hrow[t]] = t ? vh[1] : vh[0];

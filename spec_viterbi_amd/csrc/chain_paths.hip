@@ -70,11 +70,11 @@ __device__ uint32_t recompute_jstar(const BandModel& m, const FusedBatch& b, uin
         for (int off = 32; off >= 1; off >>= 1) pm = fminf(pm, __shfl_xor(pm, off));
         const float* tl = e + cap;  // heavy constants of sym[i]
         float n0 = tl[kBandTailA + 0] + pm;
-        n0 = fminf(n0, tl[kBandTailX + 0] + vh0);
-        n0 = fminf(n0, tl[kBandTailX + 1] + vh1);
+        n0 = fminf(n0, tl[band_tail_x(0, 0)] + vh0);
+        n0 = fminf(n0, tl[band_tail_x(0, 1)] + vh1);
         float n1 = tl[kBandTailA + 1] + pm;
-        n1 = fminf(n1, tl[kBandTailX + kBandHeavy] + vh0);
-        n1 = fminf(n1, tl[kBandTailX + kBandHeavy + 1] + vh1);
+        n1 = fminf(n1, tl[band_tail_x(1, 0)] + vh0);
+        n1 = fminf(n1, tl[band_tail_x(1, 1)] + vh1);
         vh0 = n0;
         vh1 = n1;
         float* tmp = cur;
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
 #pragma unroll
             for (int k = 0; k < kBandHeavy; ++k) {
                 if ((m.hx_exist >> (h * kBandHeavy + k)) & 1u) {
-                    const float val = tl[kBandTailX + h * kBandHeavy + k] + vo[k];
+                    const float val = tl[band_tail_x(h, k)] + vo[k];
                     const uint32_t col = (uint32_t)m.hrow[k];
                     const bool take = !hex || val < hv || (val == hv && col < hcol);
                     hv = take ? val : hv;

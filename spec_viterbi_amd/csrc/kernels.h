@@ -91,6 +91,10 @@ constexpr int kBandTailA = 0;
 constexpr int kBandTailX = kBandHeavy;
 constexpr int kBandTailE = kBandHeavy + kBandHeavy * kBandHeavy;
 constexpr int kBandTail = 8;  // floats (>= kBandTailE + kBandHeavy, multiple of 4)
+// X[h][k] (heavy row k -> heavy row h) in the tail: diagonal pair first, then the off-diagonal
+// pair, so each is one aligned f32 pair for v_pk_add_f32: [A0 A1 | X00 X11 | X01 X10 | E0 E1].
+constexpr int band_tail_x(int h, int k) { return kBandTailX + (h == k ? h : kBandHeavy + h); }
+static_assert(kBandHeavy == 2, "band_tail_x assumes two heavy rows");
 static_assert(kBandTailE + kBandHeavy <= kBandTail, "band row tail");
 
 struct BandModel {

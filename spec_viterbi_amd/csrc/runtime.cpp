@@ -533,7 +533,7 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge
             if (!bp.hvalid[x]) continue;
             const float eh = E[bp.hrow[x]];
             tl[kBandTailA + x] = eh + wh[x];  // fl(E_h + w_h): the shared uniform term
-            for (const auto& [src, w] : exc[x]) tl[kBandTailX + x * kBandHeavy + src] = eh + w;  // heavy src -> h
+            for (const auto& [src, w] : exc[x]) tl[band_tail_x((int)x, (int)src)] = eh + w;  // heavy src -> h
             tl[kBandTailE + x] = eh;
         }
     }
