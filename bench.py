@@ -40,7 +40,7 @@ DATA = os.path.join(ROOT, "data")
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_GHZ = 2.4         # MI355X_MICROARCH.md: max shader clock
-KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain"}
+KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain", 5: "pipe"}
 
 
 def parse(argv=None):
@@ -201,8 +201,8 @@ def cpu_baseline(hmm, seqs, seconds: float) -> dict:
 
 # ---- rocprofv3 PMC passes (children on tools/launch.py) ---------------------------------------
 PMC_PASSES = {
-    "sq": ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY",
-           "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE"],
+    "sq": ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+           "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE"],
     "fetch": ["FETCH_SIZE"],
     "write": ["WRITE_SIZE"],
 }
@@ -240,17 +240,23 @@ def pmc_counters(launch_args: list[str], kernel_prefix: str) -> dict | None:
 
 
 def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc) -> dict:
-    """VALU-issue roofline of the chain kernel (the per-observation step is VALU + LDS work on
+    """VALU-issue roofline of the step kernels (the per-observation step is VALU + LDS work on
     registers; HBM carries only symbols in and scores out).  Capacity of one SIMD-32: one wave64
     VALU instruction per 2 cycles, and at most one per 4 cycles from a single wave
     (MI355X_MICROARCH.md, cycle constants), so a SIMD holding w waves issues min(w/4, 1/2) per
     cycle.  Peak = the SIMDs the launch occupies x that rate x 2.4 GHz; achieved = SQ_INSTS_VALU
-    per launch / HIP-event kernel time."""
+    per launch / HIP-event kernel time.  The pipelined kernel runs nseq x pipe_groups workgroups
+    of pipe_waves waves; `issue_frac_all` also counts its SALU and LDS instructions, which take a
+    wave's issue slot the same way (its bound at one wave per SIMD)."""
     waves_per_wg = max(1, int(plan["threads"]) // 64)
+    pipe = plan["kernel"] == 5
     wide = plan["threads"] == info.get("wide_threads") and plan["slots"] == info.get("wide_slots") and nseq > info["cu_count"]
     wg_per_cu = 4 if wide else 1  # launch-bounds occupancy of the wide plan; one WG per CU otherwise
-    cus = min(info["cu_count"], -(-nseq // wg_per_cu)) if info["cu_count"] else 256
-    waves_per_simd = min(8, waves_per_wg * min(wg_per_cu, -(-nseq // max(cus, 1))) / 4.0)
+    wgs = nseq * int(info.get("pipe_groups", 1)) if pipe else nseq
+    if pipe:
+        wg_per_cu = max(1, -(-wgs // max(info["cu_count"], 1)))
+    cus = min(info["cu_count"], -(-wgs // wg_per_cu)) if info["cu_count"] else 256
+    waves_per_simd = min(8, waves_per_wg * min(wg_per_cu, -(-wgs // max(cus, 1))) / 4.0)
     rate = min(waves_per_simd / 4.0, 0.5)  # wave-instructions per cycle per SIMD
     peak = cus * 4 * rate * CLOCK_GHZ  # G wave-instructions / s
     res = {"bound": "valu_issue", "unit": "G VALU wave-instr/s", "peak": round(peak, 2),
@@ -266,6 +272,11 @@ def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc) -> dict:
         res["achieved"] = round(ach, 2)
         res["frac"] = round(ach / peak, 4)
         res["valu_per_wave"] = round(pmc["SQ_INSTS_VALU"] / max(pmc.get("SQ_WAVES", 1), 1), 1)
+        if "SQ_INSTS_SALU" in pmc and "SQ_INSTS_LDS" in pmc:
+            allins = pmc["SQ_INSTS_VALU"] + pmc["SQ_INSTS_SALU"] + pmc["SQ_INSTS_LDS"]
+            one_wave = cus * 4 * min(waves_per_simd, 1.0) * 0.25 * CLOCK_GHZ  # 1 instr / 4 cycles / wave
+            res["issue_all_G_per_s"] = round(allins / (kernel_ms * 1e-3) / 1e9, 2)
+            res["issue_frac_all"] = round(res["issue_all_G_per_s"] / max(one_wave, 1e-9), 4) if waves_per_simd <= 1 else None
         if "SQ_WAVE_CYCLES" in pmc and "SQ_WAVES" in pmc:  # quad-cycles
             res["wave_cycles"] = round(4 * pmc["SQ_WAVE_CYCLES"] / pmc["SQ_WAVES"], 0)
             res["wait_frac"] = round(pmc.get("SQ_WAIT_ANY", 0) / pmc["SQ_WAVE_CYCLES"], 4)
@@ -369,6 +380,8 @@ def main(argv=None):
     kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, stops)]))
 
     scores = batch.read(sptr)[0] if batch else np.zeros((0, n), np.float32)
+    # rows of the last timed pass the pipelined kernel handed to the serial kernel (0 expected)
+    fallbacks = batch.fallbacks() if batch else 0
     # correctness guard on the timed output (rank 0 vs the committed goldens of sequences 0..1)
     golden_checked = False
     if (rank == 0 and not args.no_check and args.shard == "none" and args.model == "2405.chmm"
@@ -412,10 +425,11 @@ def main(argv=None):
                  else "spec_chunk+" + KERNEL_NAMES.get(plan["kernel"], "?") if args.level >= 2
                  else KERNEL_NAMES.get(plan["kernel"], "?"))
         pmc = None
-        if not args.no_pmc and world == 1 and args.level <= 1 and not args.paths and plan["kernel"] == 4:
+        if not args.no_pmc and world == 1 and args.level <= 1 and not args.paths and plan["kernel"] in (4, 5):
             largs = ["--model", args.model, "--ess", ess_name, "--replicate", str(args.replicate), "--steps", "3",
                      "--warmup", "1"]
-            pmc = pmc_counters(largs, "void svh::(anonymous namespace)::chain_viterbi_kernel")
+            kpref = "chain_viterbi_kernel" if plan["kernel"] == 4 else "pipe_viterbi_kernel"
+            pmc = pmc_counters(largs, "void svh::(anonymous namespace)::" + kpref)
         rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc)
         workload = (f"{args.model} x {ess_name}" +
                     (f" x{args.replicate} (file sequences + same-shape synthetic copies)" if args.replicate > 1 else "") +
@@ -438,6 +452,8 @@ def main(argv=None):
                 "workload": workload, "states": n, "nnz": nnz, "sequences_per_gpu": len(seqs),
                 "observations_per_gpu": sum(lengths), "state_updates_per_gpu": updates_per_rank, "level": args.level,
                 "kernel": kname, "threads": plan["threads"], "slots": plan["slots"], "paths": bool(args.paths),
+                "workgroups_per_sequence": int(info["pipe_groups"]) if plan["kernel"] == 5 else 1,
+                "fallback_rows": fallbacks,
                 "heavy_rows": plan["heavy_rows"], "spec_prep_s": None if prep_s is None else round(prep_s, 4),
                 "golden_checked": golden_checked,
                 "parallelism": (f"LPT sequence shards x{world}, one RCCL gather of scores after timing" if args.shard == "covid"

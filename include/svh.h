@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SVH_ABI_VERSION 1
+#define SVH_ABI_VERSION 2  /* 2: svh_model_info pipe_* fields, SVH_KERNEL_PIPE, svh_batch_fallbacks */
 
 enum {
     SVH_OK = 0,
@@ -71,7 +71,12 @@ void svh_ess_free(svh_ess_t e);
  * is chain-shaped with at most one heavy row feeding the light rows (every reference .chmm), else
  * the fused (or generic) kernel with 16-bit backpointers. */
 enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2, SVH_KERNEL_BAND = 3,
-       SVH_KERNEL_CHAIN = 4 };
+       SVH_KERNEL_CHAIN = 4, SVH_KERNEL_PIPE = 5 };
+/* PIPE: the pipelined chain kernel (MSV-shaped models whose feeder row N takes terms only from
+ * the light rows and itself): a sequence's states are split over many waves and CUs; N's light
+ * term is speculated away and checked exactly at every observation, and a sequence that fails
+ * the check is re-run by the serial chain kernel (same results either way).  AUTO uses it for
+ * scores-only passes over batches too small to fill the chip with the chain kernel. */
 
 typedef struct {
     int32_t device;      /* HIP device ordinal; -1 = the caller's current device */
@@ -108,6 +113,10 @@ typedef struct {
                               workgroups per CU): its threads per workgroup, 0 = none */
     int32_t wide_slots;    /* ... and its states per thread */
     uint32_t cu_count;     /* CUs of the model's device: batches of more sequences switch plans */
+    int32_t pipe_slots;    /* pipelined plan (SVH_KERNEL_PIPE): states per lane, 0 = none */
+    int32_t pipe_waves;    /* ... waves per workgroup */
+    int32_t pipe_groups;   /* ... workgroups per sequence */
+    uint32_t pipe_max_nseq; /* AUTO runs the pipelined plan for batches of at most this many sequences */
 } svh_model_info;
 /* The model's plan for a one-sequence scores-only run (kernel/threads/slots describe it). */
 int svh_model_get_info(svh_model_t m, svh_model_info* info);
@@ -152,6 +161,10 @@ int svh_batch_elapsed_ms(svh_batch_t b, float* ms);
 /* The plan svh_batch_run(level) launches for this batch (its sequence count and paths flag
  * decide between the narrow and the wide chain plan): kernel/threads/slots of the model info. */
 int svh_batch_plan(svh_batch_t b, uint32_t level, svh_model_info* info);
+/* Rows of the last run whose pipelined pass (SVH_KERNEL_PIPE) failed its speculation check and
+ * were re-run by the serial chain kernel (results are identical either way); 0 if the last run
+ * did not use the pipelined kernel.  Waits for the run. */
+int svh_batch_fallbacks(svh_batch_t b, uint64_t* rows);
 int svh_batch_destroy(svh_batch_t b);
 
 /* Batch from uint8 symbols (the device format; e.g. straight from svh_reader_next). */

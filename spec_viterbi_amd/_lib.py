@@ -30,6 +30,7 @@ SVH_KERNEL_FUSED = 1
 SVH_KERNEL_GENERIC = 2
 SVH_KERNEL_BAND = 3
 SVH_KERNEL_CHAIN = 4
+SVH_KERNEL_PIPE = 5
 SVH_BATCH_PATHS = 1
 
 
@@ -51,7 +52,8 @@ class svh_model_info(ctypes.Structure):
         ("light_terms", c_int32), ("heavy_rows", c_int32), ("heavy_uniform", c_int32), ("device", c_int32),
         ("n", c_uint64), ("S", c_uint64), ("nnz", c_uint64), ("lds_bytes", c_uint64),
         ("spec_level", c_uint64), ("spec_bytes", c_uint64), ("paths_kernel", c_int32), ("wide_threads", c_int32),
-        ("wide_slots", c_int32), ("cu_count", c_uint32),
+        ("wide_slots", c_int32), ("cu_count", c_uint32), ("pipe_slots", c_int32), ("pipe_waves", c_int32),
+        ("pipe_groups", c_int32), ("pipe_max_nseq", c_uint32),
     ]
 
 
@@ -84,6 +86,7 @@ SIGNATURES = {
     "svh_batch_device_results": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
     "svh_batch_elapsed_ms": (c_int, [c_void_p, P_f32]),
     "svh_batch_plan": (c_int, [c_void_p, c_uint32, POINTER(svh_model_info)]),
+    "svh_batch_fallbacks": (c_int, [c_void_p, P_u64]),
     "svh_batch_destroy": (c_int, [c_void_p]),
     "svh_viterbi": (c_int, [c_void_p, c_uint32, c_uint64, P_u64, P_u64, P_f32, P_i64, P_i32]),
     "svh_batch_create_u8": (c_int, [c_void_p, c_uint64, P_u64, POINTER(ctypes.c_uint8), c_uint32, POINTER(c_void_p)]),

@@ -65,6 +65,7 @@ __global__ __launch_bounds__(kMaxBandThreads) void band_viterbi_kernel(BandModel
 
     const uint32_t B = m.B, n = m.n, erow = m.erow, W = B >> 6;
     const uint32_t t = threadIdx.x, lane = t & 63u, q = blockIdx.x;
+    if (b.run_mask && b.run_mask[q] == 0) return;  // fallback pass: only the marked rows
     const uint32_t wave = (uint32_t)uniform((int)(t >> 6));  // wave-uniform: scalar DMA loop and waits
     const uint32_t tail = SM * B;
     const float* __restrict__ erows = m.erows;

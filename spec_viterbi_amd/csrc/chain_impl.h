@@ -184,6 +184,7 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
     const uint32_t n = m.n, erow = m.erow, S = m.S;
     const uint32_t t = threadIdx.x, lane = t & 63u, q = blockIdx.x;
     const uint32_t wave = (uint32_t)uniform((int)(t >> 6));
+    if (b.run_mask && b.run_mask[q] == 0) return;  // fallback pass: only the marked rows
     constexpr uint32_t tail = SM * B;
     // diagnostic ablations (never planned): 1 = lane 63 alone publishes, 2 = no arrival check
     // of the partial cells, 4 = no tag check of the boundary words (2 and 4 give wrong results)

@@ -71,6 +71,10 @@ struct FusedBatch {
     const uint64_t* hrec_off;   // [nseq] u32 offset of sequence q's records
     float* ckpt;
     const uint64_t* ckpt_off;   // [nseq] float offset of sequence q's checkpoint rows
+    // Fallback pass after the pipelined kernel (pipe.hip): when set, only rows with
+    // run_mask[q] != 0 run (the others return at once).  Step kernels check it first.
+    const uint32_t* run_mask;
+    const struct PipeScratch* pipe;  // host side only: scratch of the pipelined kernel (nullable)
     uint32_t nseq;
 };
 
@@ -160,6 +164,54 @@ constexpr uint32_t kCkptEvery = 16;
 inline uint64_t chain_ckpt_floats(uint64_t len, uint32_t sm, uint32_t threads) {
     return len ? ((len - 1) / kCkptEvery + 1) * (uint64_t)sm * threads : 0;
 }
+
+// Pipelined chain kernel (pipe.hip): MSV-shaped models whose one heavy feeder F (the rows' N) and
+// sink S (C) satisfy: light rows take terms from position p-1 and from F only; F from the light
+// rows (one shared weight) and itself; S from the light rows (one shared weight), itself and F.
+// F's light term is speculated away -- F'(t) = fl(X_FF(o_t) + F'(t-1)) -- which removes the
+// per-observation all-position reduction from the recurrence: a sequence's positions are cut
+// into blocks of 64*SM that run as a pipeline of waves (each wave sweeps every observation of
+// its block and streams its last position's score to the next block's wave: LDS within a
+// workgroup, 8-byte tagged granules through L2 between workgroups).  Every lane checks the
+// speculation exactly at every observation (fl(A_F(o_t) + min of its light scores at t-1) <
+// F'(t) would have changed F); a sequence that fails it is re-run by the serial chain kernel.
+// S is exact without any reduction: its update is monotone in the light scores, so
+// S(t) = min over lanes of a per-lane S recurrence driven by the lane's own scores.
+constexpr int kPipeRing = 32;       // LDS ring (observations) between the waves of a workgroup
+constexpr int kPipeGroup = 8;       // observations per exchange group
+constexpr int kPipeGRing = 256;     // L2 granule ring (observations) between workgroups
+constexpr int kPipeAhead = 4;       // granule groups a consumer keeps in flight
+constexpr int kPipeWindow = 1024;   // symbols per VGPR window (64 lanes x 16 B)
+struct PipeModel {
+    const float2* tab;      // [nblk][S][SM][64]: (fl(E_o[p] + bw_p), fl(E_o[p] + aw_p)), +inf pad
+    const float* e0;        // [S][P]: E_o[row of position p] (the first observation)
+    const float* start;     // [P]: start score of position p (+inf pad)
+    const uint32_t* lrow;   // [P]: row id of position p (0xFFFFFFFF pad)
+    const float* hc;        // [S][8]: A_S A_F X_SS X_FF | X_SF E_F E_S 0 (fl(E_o[h] + w) each)
+    int rowF, rowS;         // heavy rows (rowS < 0: the model has no sink row)
+    float startF, startS;
+    uint32_t n, S, P, nblk, SM, W, G;  // P = nblk*64*SM positions, G workgroups per sequence
+    uint32_t sx;            // S has a term from F
+    uint32_t* fault;        // set non-zero if a bounded wait gave up
+    unsigned long long* stamps;  // diagnostics (SVH_PIPE_DEBUG): [ticket][W][8] counters, or null
+};
+constexpr int kPipeStamps = 8;
+// Per-batch scratch of the pipelined kernel (sized for `rows` rows).
+struct PipeScratch {
+    uint32_t* ctr;    // [4]: [0] workgroup ticket, [1] finished workgroups, [2] last epoch
+    uint32_t* done;   // [rows] finished workgroups of row q (reset by its last one)
+    uint64_t* part;   // [rows][G][2]: {C min | violation, (best value, best row) key}
+    uint64_t* gran;   // [rows][G-1][kPipeGRing] tagged boundary granules {score, tag}
+    uint32_t* cons;   // [rows][G] granules received by workgroup g's first wave
+    uint32_t* viol;   // [rows] 1: speculation failed, row needs the serial kernel
+    uint32_t rows, G;
+};
+inline size_t pipe_lds_bytes(uint32_t W, uint32_t S) {
+    // boundary ring [W][kPipeRing][64] | counters [16] | heavy constants [S][8] | reduction [W][4] | ticket
+    return ((size_t)W * kPipeRing * 64 + 16 + (size_t)S * 8 + (size_t)W * 4 + 4) * 4;
+}
+bool pipe_supported(int sm, int waves, bool sx);
+hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
 
 // CSR of T^T used by the generic kernel and the _spec precompute.
 struct CsrModel {

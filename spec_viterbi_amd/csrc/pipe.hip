@@ -1,0 +1,645 @@
+// Pipelined chain Viterbi kernel (gfx950): the latency path for MSV-shaped models whose feeder row
+// F (N) is speculated and verified exactly (kernels.h, PipeModel).
+//
+// Reference hot loop: Viterbi_impl/GraphBLAS_impl.cpp:59-73 (same association, bit-identical):
+//     v'[j] = min_k fl( fl(E[o][j] + T^T[j][k]) + v[k] )
+// For the light rows of the chain shape this is v'_p = min(fl(eb_p(o) + v_{p-1}), fl(ea_p(o) + F))
+// with eb_p(o) = fl(E_o[p] + bw_p), ea_p(o) = fl(E_o[p] + aw_p) (the reference's first add, folded
+// into the table), so once F's sequence is known a position depends only on its chain predecessor
+// one observation earlier: a wavefront over (position block, observation) with no feedback.
+//
+// Geometry: block b = 64*SM consecutive positions, one wave (lane l holds positions
+// b*64*SM + l*SM + s); W blocks per workgroup, G = ceil(nblk / W) workgroups per sequence.
+// Each wave sweeps all observations of its block.  Its last position's score of observation t
+// is the chain input of the next block's position 0 at t+1:
+//   * within a workgroup: every lane writes its score into an LDS ring [kPipeRing][64] each
+//     observation; the wave publishes "observations done" once per group of 8; the consumer
+//     waits for the whole group, reads its 8 boundary values with one ds_read and extracts them
+//     with v_readlane (one per observation); producers check the consumer's count once per
+//     group before reusing ring slots.
+//   * between workgroups: the last wave stores 8-byte granules {score, tag} (agent scope, sc1)
+//     into a ring of kPipeGRing per sequence boundary; the next workgroup's first wave keeps
+//     kPipeAhead groups of granule loads in flight and checks the tags; flow control through a
+//     tagged progress word.  Workgroups take dynamic tickets in start order, so a consumer's
+//     producer always started first (no deadlock when the grid exceeds residency).
+// Per lane and observation the heavy side is: S partial  c' = min(fl(A_S + m), fl(X_SS + c)
+// [, fl(X_SF + F)]) with m = min of the lane's scores at t-1 (exact: S(t) = min over lanes of c,
+// fl(a + .) is monotone), F' = fl(X_FF + F), and the check fl(A_F + m) < F' (a violation: F
+// would have taken its light term, the speculation and everything after it is void).
+// The last workgroup of a sequence to finish combines the partials (S, argmin, violation).
+#include "device_common.h"
+#include "kernels.h"
+
+namespace svh {
+
+using namespace dev;
+
+namespace {
+
+typedef float f32x32 __attribute__((ext_vector_type(32)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+constexpr uint32_t kR = kPipeRing;
+constexpr uint32_t kGR = kPipeGRing;
+constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t lds_ld32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Agent-scope relaxed accesses: global_load / global_store ... sc1 (L2-coherent, bypass L1).
+__device__ __forceinline__ uint64_t g_ld64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_st64(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One lane's LDS store of a wave-uniform word: EXEC narrowed to lane 0 inside the asm (no
+// divergent branch in the compiler's view).
+__device__ __forceinline__ void lds_put1(uint32_t addr, uint32_t v) {
+    uint64_t saved;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "s_nop 1\n\t"
+        "ds_write_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "v"(addr), "v"(v)
+        : "memory");
+}
+
+// Chain and feeder terms of slot 0: xb = fl(eb + (lane ? x[lane-1] : bnd)), xa = fl(ea + f).
+// The DPP read of x follows two VALU instructions of this block (its two wait states).
+__device__ __forceinline__ void chain_terms(float& xb, float& xa, float eb, float ea, float bnd, float f,
+                                            float x) {
+    asm("v_add_f32_e32 %0, %2, %3\n\t"
+        "v_add_f32_e32 %1, %4, %5\n\t"
+        "v_add_f32_dpp %0, %6, %3 wave_shr:1 row_mask:0xf bank_mask:0xf"
+        : "=&v"(xb), "=&v"(xa)
+        : "s"(bnd), "v"(eb), "v"(f), "v"(ea), "v"(x));
+}
+
+// The same with lane 0's chain input taken from lane R of the group vector bvv (row_ror:16-R
+// rotates lane R of each row of 16 into its lane 0; no SGPR round trip).  xa comes first and an s_nop follows, so both DPP sources have two wait
+// states after whatever wrote them last.
+template <int R>
+__device__ __forceinline__ void chain_terms_v(float& xb, float& xa, float eb, float ea, float bvv, float f,
+                                              float x) {
+    if constexpr (R == 0) {
+        asm("v_add_f32_e32 %1, %4, %5\n\t"
+            "v_add_f32_e32 %0, %2, %3\n\t"
+            "v_add_f32_dpp %0, %6, %3 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb), "=&v"(xa)
+            : "v"(bvv), "v"(eb), "v"(f), "v"(ea), "v"(x));
+    } else {
+        asm("v_add_f32_e32 %1, %4, %5\n\t"
+            "s_nop 0\n\t"
+            "v_add_f32_dpp %0, %2, %3 row_ror:%7 row_mask:0xf bank_mask:0xf\n\t"
+            "v_add_f32_dpp %0, %6, %3 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb), "=&v"(xa)
+            : "v"(bvv), "v"(eb), "v"(f), "v"(ea), "v"(x), "n"(16 - R));  // lane 0 <- lane R
+    }
+}
+
+__device__ __forceinline__ float readlane_f(float x, uint32_t l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), (int)l));
+}
+__device__ __forceinline__ uint32_t readlane_u(uint32_t x, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
+}
+
+// Granule tag of observation s in this launch: epoch and ring lap (a slot is rewritten every
+// kGR observations; flow control keeps the consumer within one lap).
+__device__ __forceinline__ uint32_t gtag(uint32_t ep, uint32_t s) {
+    return ((ep % 0xFFFFFu + 1u) << 12) | ((s >> 8) & 0xFFFu);  // never 0 (zeroed memory)
+}
+static_assert(kGR == 256, "gtag assumes a 256-slot ring");
+
+// Granule prefetch into a register the loop carries (tied operand: no copy at the back edge, so
+// no wait is forced there); the caller waits with an explicit vmcnt before reading it.
+__device__ __forceinline__ void g_prefetch64(uint64_t& dst, const uint64_t* p) {
+    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "+v"(dst) : "v"(p) : "memory");
+}
+
+template <int SM, int W, bool SX>
+__global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* ring = lds;                                                  // [W][kR][64]
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(ring + W * kR * 64);    // [16]
+    float* ctab = reinterpret_cast<float*>(cnt + 16);                   // [S][8]
+    float* red = ctab + m.S * 8;                                        // [W][4]
+    uint32_t* tick = reinterpret_cast<uint32_t*>(red + W * 4);
+
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t w = (uint32_t)uniform((int)(tid >> 6));
+    const uint32_t S = m.S, P = m.P, G = m.G;
+    if (tid == 0) *tick = __hip_atomic_fetch_add(x.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 16) cnt[tid] = 0;
+    for (uint32_t i = tid; i < S * 8; i += 64 * W) ctab[i] = m.hc[i];
+    __syncthreads();
+    const uint32_t id = (uint32_t)uniform((int)*tick);
+    const uint32_t q = id / G, g = id - q * G;
+    const uint32_t ep = (uint32_t)uniform((int)__hip_atomic_load(x.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+
+    const uint8_t* __restrict__ sym = b.symbols + b.sym_off[q];
+    const uint32_t len = (uint32_t)uniform((int)b.end[q]);
+    const uint32_t beg = (uint32_t)uniform((int)b.begin[q]);
+    const uint32_t first = beg ? beg : 1u;  // first observation the steps run (state at first-1)
+    const uint32_t blk = g * W + w;
+    const bool act = blk < m.nblk;
+    const bool lastb = blk + 1 >= m.nblk;
+    // boundary roles: source 0 none (block 0), 1 LDS (previous wave), 2 granules (previous
+    // workgroup); sink 0 none (last block), 1 LDS, 2 granules
+    const int src = blk == 0 ? 0 : (w > 0 ? 1 : 2);
+    const int dst = lastb ? 0 : (w + 1 < (uint32_t)W ? 1 : 2);
+
+    float v[SM];  // light scores of the lane's positions
+    f2 CF;        // {S partial of this lane, F'} (one register pair: the packed heavy update)
+    uint64_t viol = 0;
+    uint32_t spins = 0;
+    // diagnostics: 0 loop cycles, 1 head cycles, 2 tail cycles, 3 slow re-reads waiting for the
+    // previous wave, 4 ... for the next wave (flow control), 5 ... for granules, 6 ... for the
+    // consumer's progress word, 7 body iterations
+    unsigned long long dg[kPipeStamps] = {};
+    const bool dbg = m.stamps != nullptr;
+
+    if (act) {
+        const uint32_t p0 = blk * 64 * SM + lane * SM;
+        // ---- tables: (eb, ea) of the lane's positions for every symbol, in VGPRs
+        f32x32 EB[SM], EA[SM];
+#pragma unroll
+        for (int s = 0; s < SM; ++s)
+#pragma unroll
+            for (int o = 0; o < 32; ++o) {
+                const float2 e = (uint32_t)o < S ? m.tab[((size_t)(blk * S + o) * SM + s) * 64 + lane]
+                                                 : make_float2(kInf, kInf);
+                EB[s][o] = e.x;
+                EA[s][o] = e.y;
+            }
+        // heavy constants as lane tables (lane o: symbol o), extracted with v_readlane
+        const bool lo = lane < S;
+        const float cAS = lo ? m.hc[lane * 8 + 0] : kInf, cAF = lo ? m.hc[lane * 8 + 1] : kInf;
+        const float cXSS = lo ? m.hc[lane * 8 + 2] : kInf, cXFF = lo ? m.hc[lane * 8 + 3] : kInf;
+        const float cXSF = lo ? m.hc[lane * 8 + 4] : kInf;
+        // ---- state at observation first-1
+        if (beg == 0) {
+            const uint32_t o0 = (uint32_t)uniform((int)sym[0]);
+#pragma unroll
+            for (int s = 0; s < SM; ++s) v[s] = m.e0[(size_t)o0 * P + p0 + s] + m.start[p0 + s];
+            CF.y = m.rowF >= 0 ? ctab[o0 * 8 + 5] + m.startF : kInf;
+            CF.x = (blk == 0 && lane == 0 && m.rowS >= 0) ? ctab[o0 * 8 + 6] + m.startS : kInf;
+        } else {
+            const float* vin = b.v_in + (size_t)b.v_in_row[q] * m.n;
+#pragma unroll
+            for (int s = 0; s < SM; ++s) {
+                const uint32_t r = m.lrow[p0 + s];
+                v[s] = r != kNoRow ? vin[r] : kInf;
+            }
+            CF.y = m.rowF >= 0 ? vin[m.rowF] : kInf;
+            CF.x = (blk == 0 && lane == 0 && m.rowS >= 0) ? vin[m.rowS] : kInf;
+        }
+
+        // ---- symbols: 1024-observation windows in VGPRs (lane l: bytes 16l..16l+15)
+        const uint32_t slen = len + kSymPad;
+        auto load_window = [&](uint32_t wi) -> uint4 {
+            const uint32_t off = wi * kPipeWindow + lane * 16;
+            return off < slen ? *reinterpret_cast<const uint4*>(sym + off) : make_uint4(0, 0, 0, 0);
+        };
+        uint32_t cwi = first >> 10;
+        uint4 cw = load_window(cwi), nw = load_window(cwi + 1);
+        auto window_for = [&](uint32_t t) {  // uniform; windows advance one at a time
+            if ((t >> 10) != cwi) {
+                cw = nw;
+                ++cwi;
+                nw = load_window(cwi + 1);
+            }
+        };
+        auto sym1 = [&](uint32_t t) -> uint32_t {  // symbol of observation t (slow path)
+            const uint32_t r = t & 1023u, ln = r >> 4, d = (r >> 2) & 3u;
+            const uint32_t wd = d == 0 ? readlane_u(cw.x, ln) : d == 1 ? readlane_u(cw.y, ln)
+                              : d == 2 ? readlane_u(cw.z, ln) : readlane_u(cw.w, ln);
+            return (wd >> ((r & 3u) * 8)) & 0xFFu;
+        };
+
+        // ---- one observation with symbol o; bnd = the previous block's last score at t-1
+        auto step = [&](uint32_t o, auto chain) {
+            const float kas = readlane_f(cAS, o), kaf = readlane_f(cAF, o);
+            const float kxss = readlane_f(cXSS, o), kxff = readlane_f(cXFF, o);
+            float eb[SM], ea[SM];
+#pragma unroll
+            for (int s = 0; s < SM; ++s) {
+                eb[s] = EB[s][o];
+                ea[s] = EA[s][o];
+            }
+#pragma unroll
+            for (int s = 0; s < SM; ++s) asm volatile("" : "+v"(eb[s]), "+v"(ea[s]));  // one idx block
+            float vn[SM];
+            {
+                float xb, xa;
+                chain(xb, xa, eb[0], ea[0], CF.y, v[SM - 1]);
+                vn[0] = fminf(xa, xb);
+            }
+#pragma unroll
+            for (int s = 1; s < SM; ++s) vn[s] = fminf(ea[s] + CF.y, eb[s] + v[s - 1]);
+            // heavy side from the scores of t-1
+            float pm = v[0];
+#pragma unroll
+            for (int s = 1; s < SM; ++s) pm = fminf(pm, v[s]);
+            const f2 s1 = (f2){kas, kaf} + (f2){pm, pm};  // A_S + m, A_F + m
+            const f2 s2 = (f2){kxss, kxff} + CF;          // X_SS + c, X_FF + F
+            float cn = fminf(s1.x, s2.x);
+            if constexpr (SX) cn = fminf(cn, readlane_f(cXSF, o) + CF.y);
+            {  // viol |= [A_F + m < F'] per lane, folded at once (not held per step by the compiler)
+                uint64_t c;
+                asm volatile("v_cmp_lt_f32_e64 %1, %2, %3\n\ts_or_b64 %0, %0, %1"
+                             : "+s"(viol), "=&s"(c)
+                             : "v"(s1.y), "v"(s2.y)
+                             : "scc");
+            }
+            CF = (f2){cn, s2.y};
+#pragma unroll
+            for (int s = 0; s < SM; ++s) v[s] = vn[s];
+        };
+
+        // ---- exchange state
+        float* const ring_w = ring + w * kR * 64;
+        const float* const ring_prev = ring_w - kR * 64;
+        uint32_t* const cnt_w = cnt + w;
+        const uint32_t cnt_addr = lds_addr(cnt_w);
+        uint64_t* const gin = x.gran + ((size_t)q * (G - 1) + (g - 1)) * kGR;  // src == 2
+        uint64_t* const gout = x.gran + ((size_t)q * (G - 1) + g) * kGR;       // dst == 2
+        uint64_t* const cons_in = reinterpret_cast<uint64_t*>(x.cons) + (size_t)q * G + g;      // src == 2 publishes
+        const uint64_t* const cons_out = reinterpret_cast<const uint64_t*>(x.cons) + (size_t)q * G + g + 1;  // dst == 2 reads
+        float bprev = kInf;  // boundary score of observation t-1 for the next step (uniform)
+
+        auto give_up = [&]() -> bool { return ++spins > kSpinLimit; };
+        // wait until the previous wave has published observations < need
+        auto wait_prev = [&](uint32_t need) {
+            while ((uint32_t)uniform((int)lds_ld32(cnt_w - 1)) < need) {
+                if (dbg) ++dg[3];
+                if (give_up()) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        };
+        // flow control: the next wave has consumed observations < need
+        auto wait_next = [&](uint32_t need) {
+            while ((int)uniform((int)lds_ld32(cnt_w + 1)) < (int)need) {
+                if (dbg) ++dg[4];
+                if (give_up()) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        };
+        auto gran_value = [&](uint32_t s) -> float {  // poll the granule of observation s (uniform)
+            const uint64_t* p = gin + (s & (kGR - 1));
+            uint64_t gv = g_ld64(p);
+            while ((uint32_t)uniform((int)(uint32_t)(gv >> 32)) != gtag(ep, s)) {
+                if (dbg) ++dg[5];
+                if (give_up()) break;
+                __builtin_amdgcn_s_sleep(1);
+                gv = g_ld64(p);
+            }
+            return __builtin_bit_cast(float, (uint32_t)uniform((int)(uint32_t)gv));
+        };
+        auto cons_ok = [&](uint64_t c, uint32_t need) -> bool {  // consumer progress word vs need
+            return (uint32_t)(c >> 32) == ep && (int)(uint32_t)c >= (int)need;
+        };
+        auto uni64 = [](uint64_t c) -> uint64_t {
+            return (uint64_t)(uint32_t)uniform((int)(uint32_t)c) | ((uint64_t)(uint32_t)uniform((int)(uint32_t)(c >> 32)) << 32);
+        };
+        auto wait_cons = [&](uint32_t need) {
+            uint64_t c = g_ld64(cons_out);
+            while (!cons_ok(uni64(c), need)) {
+                if (dbg) ++dg[6];
+                if (give_up()) break;
+                __builtin_amdgcn_s_sleep(2);
+                c = g_ld64(cons_out);
+            }
+        };
+        auto put_gran1 = [&](uint32_t s, float val) {  // single observation (slow path), lane 0 stores
+            const uint64_t gv = ((uint64_t)gtag(ep, s) << 32) | __builtin_bit_cast(uint32_t, val);
+            if (lane == 0) g_st64(gout + (s & (kGR - 1)), gv);
+        };
+        auto ring_put = [&](uint32_t t, float val) { ring_w[(t & (kR - 1)) * 64 + lane] = val; };
+
+        // The sweep, with the boundary roles as compile-time constants (one code path per role).
+        auto sweep = [&](auto srcc, auto dstc) {
+            constexpr int SRC = decltype(srcc)::value, DST = decltype(dstc)::value;
+            // one observation outside the unrolled groups: per-observation waits
+            auto single = [&](uint32_t t) {
+                window_for(t);
+                const uint32_t o = (uint32_t)uniform((int)sym1(t));
+                if constexpr (DST == 1) wait_next((int)t - (int)kR + 1);
+                if constexpr (DST == 2) {
+                    if ((t & 63u) == 0) wait_cons((int)t - (int)kGR + 64);
+                }
+                step(o, [&](float& xb, float& xa, float eb, float ea, float f, float xl) {
+                    chain_terms(xb, xa, eb, ea, bprev, f, xl);
+                });
+                ring_put(t, v[SM - 1]);
+                if constexpr (DST == 2) put_gran1(t, readlane_f(v[SM - 1], 63));
+                if (t + 1 < len) {  // fetch the boundary score of t for the next step
+                    if constexpr (SRC == 1) {
+                        wait_prev(t + 1);
+                        asm volatile("" ::: "memory");
+                        bprev = readlane_f(ring_prev[(t & (kR - 1)) * 64 + 63], 0);
+                    } else if constexpr (SRC == 2) {
+                        bprev = gran_value(t);
+                    }
+                }
+                asm volatile("" ::: "memory");
+                lds_put1(cnt_addr, t + 1);
+                if constexpr (SRC == 2) {
+                    if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | (t + 1));
+                }
+            };
+
+            // publish the state at first-1 and fetch the boundary of first-1
+            ring_put(first - 1, v[SM - 1]);
+            if constexpr (DST == 2) put_gran1(first - 1, readlane_f(v[SM - 1], 63));
+            asm volatile("" ::: "memory");
+            lds_put1(cnt_addr, first);
+            if constexpr (SRC == 1) {
+                wait_prev(first);
+                asm volatile("" ::: "memory");
+                bprev = readlane_f(ring_prev[((first - 1) & (kR - 1)) * 64 + 63], 0);
+            } else if constexpr (SRC == 2) {
+                bprev = gran_value(first - 1);
+            }
+
+            uint32_t t = first;
+            unsigned long long c0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+            // head: single observations up to a multiple of 32
+            for (; t < len && (t & 31u); ++t) single(t);
+            if (dbg) {
+                const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+                dg[1] = c1 - c0;
+                c0 = c1;
+            }
+
+            // body: 32 observations per iteration, four groups of 8
+            if (t + 32 <= len) {
+                uint64_t gq[4] = {0, 0, 0, 0};  // SRC 2: granule groups in flight
+                if constexpr (SRC == 2) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) g_prefetch64(gq[j], gin + ((t + 8 * j + (lane & 7u)) & (kGR - 1)));
+                }
+                float gpend = 0.0f;    // DST 2: the previous group's boundary scores (lanes 0..7),
+                uint32_t gpend_t = 0;  // read back from the ring one group before they are stored
+                uint64_t cons_v = 0;   // DST 2: prefetched progress word of the consumer
+                if constexpr (DST == 2) cons_v = g_ld64(cons_out);
+                // counts of the neighbouring waves, read two observations before the end of a group
+                uint32_t pc_rd = 0, nc_rd = 0;
+                if constexpr (DST == 1) nc_rd = lds_ld32(cnt_w + 1);
+                // boundary vectors (lanes 0..7 = the previous block's last scores of a group's 8
+                // observations): the previous group's (lane 7 feeds the first step) and, SRC 1,
+                // the next group's, read one group ahead whenever the producer is far enough
+                float bv_prev = bprev;  // lane 7 (all lanes) = boundary of t-1
+                float bv_next = kInf;
+                bool next_ok = false;
+                for (; t + 32 <= len; t += 32) {
+                    if (dbg) ++dg[7];
+                    window_for(t);
+                    const uint32_t r = t & 1023u, ln = r >> 4;
+                    const uint64_t sw0 = (uint64_t)readlane_u(cw.x, ln) | ((uint64_t)readlane_u(cw.y, ln) << 32);
+                    const uint64_t sw1 = (uint64_t)readlane_u(cw.z, ln) | ((uint64_t)readlane_u(cw.w, ln) << 32);
+                    const uint64_t sw2 = (uint64_t)readlane_u(cw.x, ln + 1) | ((uint64_t)readlane_u(cw.y, ln + 1) << 32);
+                    const uint64_t sw3 = (uint64_t)readlane_u(cw.z, ln + 1) | ((uint64_t)readlane_u(cw.w, ln + 1) << 32);
+                    if constexpr (DST == 2) {  // granule ring flow control, once per 32 observations
+                        if (!cons_ok(uni64(cons_v), (int)t + 32 - (int)kGR + 8)) wait_cons((int)t + 32 - (int)kGR + 8);
+                        cons_v = g_ld64(cons_out);
+                    }
+                    auto group = [&](auto jc, uint64_t sw) {
+                        constexpr uint32_t j = decltype(jc)::value;
+                        const uint32_t tg = t + 8 * j;
+                        float bv = kInf;  // lanes 0..7: the previous block's last scores of tg..tg+7
+                        if constexpr (SRC == 1) {
+                            if (next_ok) {
+                                bv = bv_next;
+                            } else {
+                                wait_prev(tg + 8);
+                                asm volatile("" ::: "memory");
+                                bv = ring_prev[(8 * j + (lane & 7u)) * 64 + 63];
+                            }
+                        } else if constexpr (SRC == 2) {
+                            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // gq[j]: 3 later loads in flight
+                            uint64_t gv = gq[j];
+                            while (__builtin_amdgcn_ballot_w64((uint32_t)(gv >> 32) != gtag(ep, tg)) != 0) {
+                                if (dbg) ++dg[5];
+                                if (give_up()) break;
+                                __builtin_amdgcn_s_sleep(1);
+                                gv = g_ld64(gin + ((tg + (lane & 7u)) & (kGR - 1)));
+                            }
+                            bv = __builtin_bit_cast(float, (uint32_t)gv);
+                            g_prefetch64(gq[j], gin + ((tg + 32 + (lane & 7u)) & (kGR - 1)));
+                        }
+                        if constexpr (DST == 1) {
+                            if ((int)uniform((int)nc_rd) < (int)tg + 8 - (int)kR) wait_next((int)tg + 8 - (int)kR);
+                        }
+                        auto one = [&](auto kc) {
+                            constexpr uint32_t k = decltype(kc)::value;
+                            const uint32_t o = (uint32_t)((sw >> (8 * k)) & 0xFFu);
+                            if constexpr (k == 0) {
+                                step(o, [&](float& xb, float& xa, float eb, float ea, float f, float xl) {
+                                    chain_terms_v<7>(xb, xa, eb, ea, bv_prev, f, xl);
+                                });
+                            } else {
+                                step(o, [&](float& xb, float& xa, float eb, float ea, float f, float xl) {
+                                    chain_terms_v<(int)k - 1>(xb, xa, eb, ea, bv, f, xl);
+                                });
+                            }
+                            ring_w[(8 * j + k) * 64 + lane] = v[SM - 1];
+                            if constexpr (k == 5) {  // the counts checked at the end of the group
+                                asm volatile("" ::: "memory");
+                                if constexpr (SRC == 1) pc_rd = lds_ld32(cnt_w - 1);
+                                if constexpr (DST == 1) nc_rd = lds_ld32(cnt_w + 1);
+                            }
+                        };
+                        one(std::integral_constant<uint32_t, 0>{});
+                        one(std::integral_constant<uint32_t, 1>{});
+                        one(std::integral_constant<uint32_t, 2>{});
+                        one(std::integral_constant<uint32_t, 3>{});
+                        one(std::integral_constant<uint32_t, 4>{});
+                        one(std::integral_constant<uint32_t, 5>{});
+                        one(std::integral_constant<uint32_t, 6>{});
+                        one(std::integral_constant<uint32_t, 7>{});
+                        bv_prev = bv;
+                        asm volatile("" ::: "memory");
+                        lds_put1(cnt_addr, tg + 8);
+                        if constexpr (SRC == 1) {  // the next group's boundary vector, if published
+                            next_ok = (uint32_t)uniform((int)pc_rd) >= tg + 16;
+                            if (next_ok) bv_next = ring_prev[(((8 * j + 8) & (kR - 1)) + (lane & 7u)) * 64 + 63];
+                        }
+                        if constexpr (DST == 2) {
+                            // granules of the previous group (read back from the ring one group ago)
+                            if (gpend_t && lane < 8)
+                                g_st64(gout + ((gpend_t + lane) & (kGR - 1)),
+                                       ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
+                            gpend = ring_w[(8 * j + (lane & 7u)) * 64 + 63];
+                            gpend_t = tg;
+                        }
+                        if constexpr (SRC == 2 && j == 3) {
+                            if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | (tg + 8));
+                        }
+                    };
+                    group(std::integral_constant<uint32_t, 0>{}, sw0);
+                    group(std::integral_constant<uint32_t, 1>{}, sw1);
+                    group(std::integral_constant<uint32_t, 2>{}, sw2);
+                    group(std::integral_constant<uint32_t, 3>{}, sw3);
+                }
+                bprev = readlane_f(bv_prev, 7);
+                if constexpr (SRC == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the prefetches
+                if constexpr (DST == 2) {
+                    if (gpend_t && lane < 8)
+                        g_st64(gout + ((gpend_t + lane) & (kGR - 1)),
+                               ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
+                }
+            }
+            if (dbg) {
+                const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+                dg[0] = c1 - c0;
+                c0 = c1;
+            }
+            // tail
+            for (; t < len; ++t) single(t);
+            if (dbg) dg[2] = __builtin_amdgcn_s_memtime() - c0;
+        };
+
+        if (len > first) {
+            using I0 = std::integral_constant<int, 0>;
+            using I1 = std::integral_constant<int, 1>;
+            using I2 = std::integral_constant<int, 2>;
+            switch (src * 3 + dst) {
+                case 0: sweep(I0{}, I0{}); break;
+                case 1: sweep(I0{}, I1{}); break;
+                case 2: sweep(I0{}, I2{}); break;
+                case 3: sweep(I1{}, I0{}); break;
+                case 4: sweep(I1{}, I1{}); break;
+                case 5: sweep(I1{}, I2{}); break;
+                case 6: sweep(I2{}, I0{}); break;
+                case 7: sweep(I2{}, I1{}); break;
+                default: sweep(I2{}, I2{}); break;
+            }
+        }
+        if (dbg && lane == 0)
+            for (int k = 0; k < kPipeStamps; ++k) m.stamps[((size_t)id * W + w) * kPipeStamps + k] = dg[k];
+        if (spins > kSpinLimit && lane == 0 && m.fault) atomicOr(m.fault, 1u);
+
+        // ---- scores of the light positions and this wave's partials
+        float* out = b.scores + (size_t)q * m.n;
+        float bvv = kInf;
+        uint32_t bk = kNoRow;
+#pragma unroll
+        for (int s = 0; s < SM; ++s) {
+            const uint32_t r = m.lrow[p0 + s];
+            if (r != kNoRow) {
+                out[r] = v[s];
+                lex_min(bvv, bk, v[s], r);
+            }
+        }
+        wave_lexmin63(bvv, bk);
+        const float cmin = wave_min63(CF.x);
+        if (lane == 63) {
+            red[w * 4 + 0] = cmin;
+            red[w * 4 + 1] = bvv;
+            red[w * 4 + 2] = __builtin_bit_cast(float, bk);
+            red[w * 4 + 3] = __builtin_bit_cast(float, viol != 0 ? 1u : 0u);
+        }
+    } else if (lane == 63) {
+        red[w * 4 + 0] = kInf;
+        red[w * 4 + 1] = kInf;
+        red[w * 4 + 2] = __builtin_bit_cast(float, kNoRow);
+        red[w * 4 + 3] = 0.0f;
+    }
+    __syncthreads();
+
+    // ---- per-sequence combine (the workgroup that finishes the sequence last) and launch end
+    if (tid == 0) {
+        float cm = kInf, bvv = kInf;
+        uint32_t bk = kNoRow, vi = 0;
+        for (uint32_t u = 0; u < (uint32_t)W; ++u) {
+            cm = fminf(cm, red[u * 4 + 0]);
+            lex_min(bvv, bk, red[u * 4 + 1], __builtin_bit_cast(uint32_t, red[u * 4 + 2]));
+            vi |= __builtin_bit_cast(uint32_t, red[u * 4 + 3]);
+        }
+        uint64_t* part = x.part + ((size_t)q * G + g) * 2;
+        g_st64(part, ((uint64_t)vi << 32) | __builtin_bit_cast(uint32_t, cm));
+        g_st64(part + 1, lex_key(bvv, bk));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t d = __hip_atomic_fetch_add(x.done + q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == G - 1) {
+            float C = kInf;
+            uint64_t key = ~0ull;
+            vi = 0;
+            for (uint32_t u = 0; u < G; ++u) {
+                const uint64_t* pu = x.part + ((size_t)q * G + u) * 2;
+                const uint64_t a = g_ld64(pu), k2 = g_ld64(pu + 1);
+                C = fminf(C, __builtin_bit_cast(float, (uint32_t)a));
+                vi |= (uint32_t)(a >> 32);
+                key = k2 < key ? k2 : key;
+            }
+            float* out = b.scores + (size_t)q * m.n;
+            float bv2 = lex_key_value(key);
+            uint32_t bk2 = lex_key_index(key);
+            if (key == ~0ull) {
+                bv2 = kInf;
+                bk2 = kNoRow;
+            }
+            if (m.rowF >= 0) {
+                out[m.rowF] = CF.y;
+                lex_min(bv2, bk2, CF.y, (uint32_t)m.rowF);
+            }
+            if (m.rowS >= 0) {
+                out[m.rowS] = C;
+                lex_min(bv2, bk2, C, (uint32_t)m.rowS);
+            }
+            if (b.best) b.best[q] = bk2 == kNoRow ? -1 : (int64_t)bk2;
+            x.viol[q] = vi;
+            __hip_atomic_store(x.done + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint32_t f = __hip_atomic_fetch_add(x.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (f == gridDim.x - 1) {  // every workgroup has taken its ticket and read the epoch
+            __hip_atomic_store(x.ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(x.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(x.ctr + 2, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <int SM, int W>
+const void* pipe_ptr(bool sx) {
+    return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<SM, W, true>)
+              : reinterpret_cast<const void*>(&pipe_viterbi_kernel<SM, W, false>);
+}
+
+const void* pipe_fn(int sm, int waves, bool sx) {
+    switch (sm * 100 + waves) {
+        case 104: return pipe_ptr<1, 4>(sx);
+        case 108: return pipe_ptr<1, 8>(sx);
+        case 204: return pipe_ptr<2, 4>(sx);
+        case 208: return pipe_ptr<2, 8>(sx);
+        default: return nullptr;
+    }
+}
+
+}  // namespace
+
+bool pipe_supported(int sm, int waves, bool sx) { return pipe_fn(sm, waves, sx) != nullptr; }
+
+hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream) {
+    const void* fn = pipe_fn((int)m.SM, (int)m.W, m.sx != 0);
+    if (!fn || m.S > 32 || m.G == 0 || m.nblk > m.G * m.W || m.P != m.nblk * 64 * m.SM || !x.ctr ||
+        b.nseq > x.rows || x.G < m.G)
+        return hipErrorInvalidValue;
+    if (b.nseq == 0) return hipSuccess;
+    PipeModel mm = m;
+    FusedBatch bb = b;
+    PipeScratch xx = x;
+    void* args[] = {&mm, &bb, &xx};
+    const uint64_t grid = (uint64_t)b.nseq * m.G;
+    if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    return hipLaunchKernel(fn, dim3((uint32_t)grid), dim3(64 * m.W), args, pipe_lds_bytes(m.W, m.S), stream);
+}
+
+}  // namespace svh

@@ -352,17 +352,28 @@ bool band_heavy_rows(const HostModel& hm, std::vector<uint32_t>* heavy_out) {
     return false;
 }
 
-}  // namespace
+// Structure of a chain-shaped model (shared by the chain / band plans and the pipelined plan).
+// Heavy rows are renumbered x = 0.. with the feeders of light rows first.
+struct BandShape {
+    bool ok = false;
+    std::vector<uint32_t> heavy;               // heavy row ids, in renumbered order x
+    std::vector<uint32_t> light;               // light row ids by position p
+    uint32_t HA = 0;                           // heavy rows feeding light rows (x < HA)
+    std::vector<float> bw;                     // [p] weight of the term from position p-1 (+inf: none)
+    std::vector<uint8_t> bex;                  // [p] that term exists
+    std::vector<std::vector<float>> aw;        // [x][p] weight of the term from heavy row x
+    std::vector<std::vector<uint8_t>> aex;     // [x][p] that term exists
+    float wh[kBandHeavy] = {kInfH, kInfH};     // shared weight of the light terms of heavy row x
+    std::vector<std::pair<uint32_t, float>> exc[kBandHeavy];  // heavy row x's terms from heavy rows
+    uint32_t hl_exist = 0, hx_exist = 0;       // BandModel::hl_exist / hx_exist
+};
 
-BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge_waves) {
-    BandPlan bp;
-    const uint32_t n = hm.n, S = hm.S;
-    if (chain && S > (uint32_t)kChainMaxSym) return bp;
-    if (max_threads <= 0) max_threads = chain ? kChainMaxThreads : kDefaultBandThreads;
-    max_threads = std::min(max_threads, chain ? kChainMaxThreads : kMaxBandThreads);
+BandShape analyze_band(const HostModel& hm) {
+    BandShape sh;
+    const uint32_t n = hm.n;
     std::vector<uint32_t> heavy;
-    if (!band_heavy_rows(hm, &heavy)) return bp;
-    if (heavy.size() > (size_t)kBandHeavy || heavy.size() >= n) return bp;
+    if (!band_heavy_rows(hm, &heavy)) return sh;
+    if (heavy.size() > (size_t)kBandHeavy || heavy.size() >= n) return sh;
     std::vector<int> hidx(n, -1);
     for (size_t h = 0; h < heavy.size(); ++h) hidx[heavy[h]] = (int)h;
     std::vector<uint32_t> light, pos(n, 0xFFFFFFFFu);
@@ -391,7 +402,7 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge
                 bwp[p] = hm.val[e];
                 bex[p] = 1;
             } else {
-                return bp;
+                return sh;
             }
         }
     }
@@ -405,8 +416,6 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge
     std::vector<int> newidx(heavy.size());
     for (size_t x = 0; x < order.size(); ++x) newidx[order[x]] = (int)x;
 
-    float wh[kBandHeavy] = {kInfH, kInfH};
-    std::vector<std::pair<uint32_t, float>> exc[kBandHeavy];
     for (size_t x = 0; x < order.size(); ++x) {
         const uint32_t j = heavy[order[x]];
         uint32_t nlight = 0;
@@ -415,7 +424,7 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge
         for (uint32_t e = hm.rowptr[j]; e < hm.rowptr[j + 1]; ++e) {
             const uint32_t k = hm.col[e];
             if (hidx[k] >= 0) {
-                exc[x].push_back({(uint32_t)newidx[hidx[k]], hm.val[e]});
+                sh.exc[x].push_back({(uint32_t)newidx[hidx[k]], hm.val[e]});
             } else {
                 ++nlight;
                 if (first) w = hm.val[e];
@@ -423,12 +432,42 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge
                 first = false;
             }
         }
-        if (exc[x].size() > (size_t)kBandHeavy) return bp;  // cannot happen: one term per source
-        if (nlight != 0 && (nlight != nL || !same)) return bp;
-        wh[x] = nlight ? w : kInfH;
-        if (nlight) bp.hl_exist |= 1u << x;
-        for (const auto& e : exc[x]) bp.hx_exist |= 1u << (x * kBandHeavy + e.first);
+        if (sh.exc[x].size() > (size_t)kBandHeavy) return sh;  // cannot happen: one term per source
+        if (nlight != 0 && (nlight != nL || !same)) return sh;
+        sh.wh[x] = nlight ? w : kInfH;
+        if (nlight) sh.hl_exist |= 1u << x;
+        for (const auto& e : sh.exc[x]) sh.hx_exist |= 1u << (x * kBandHeavy + e.first);
     }
+    for (size_t x = 0; x < order.size(); ++x) {
+        sh.heavy.push_back(heavy[order[x]]);
+        sh.aw.push_back(std::move(awp[order[x]]));
+        sh.aex.push_back(std::move(aex[order[x]]));
+    }
+    sh.light = std::move(light);
+    sh.HA = HA;
+    sh.bw = std::move(bwp);
+    sh.bex = std::move(bex);
+    sh.ok = true;
+    return sh;
+}
+
+}  // namespace
+
+BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge_waves) {
+    BandPlan bp;
+    const uint32_t n = hm.n, S = hm.S;
+    if (chain && S > (uint32_t)kChainMaxSym) return bp;
+    if (max_threads <= 0) max_threads = chain ? kChainMaxThreads : kDefaultBandThreads;
+    max_threads = std::min(max_threads, chain ? kChainMaxThreads : kMaxBandThreads);
+    BandShape sh = analyze_band(hm);
+    if (!sh.ok) return bp;
+    const std::vector<uint32_t>& light = sh.light;
+    const uint32_t nL = (uint32_t)light.size();
+    const uint32_t HA = sh.HA;
+    const float* wh = sh.wh;
+    const auto& exc = sh.exc;
+    bp.hl_exist = sh.hl_exist;
+    bp.hx_exist = sh.hx_exist;
 
     uint32_t SM = 0, B = 0;
     bool ge = false;
@@ -480,15 +519,15 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge
     bp.B = B;
     bp.SM = SM;
     bp.HA = HA;
-    bp.H = (uint32_t)heavy.size();
+    bp.H = (uint32_t)sh.heavy.size();
     bp.nL = nL;
     bp.erow = erow;
     bp.lds_bytes = band_lds_bytes(erow);
     for (int x = 0; x < kBandHeavy; ++x) {
-        const bool real = (size_t)x < order.size();
-        bp.hrow[x] = real ? (int)heavy[order[x]] : 0;
+        const bool real = (size_t)x < sh.heavy.size();
+        bp.hrow[x] = real ? (int)sh.heavy[x] : 0;
         bp.hvalid[x] = real ? 1 : 0;
-        bp.hstart[x] = real ? hm.start[heavy[order[x]]] : kInfH;
+        bp.hstart[x] = real ? hm.start[sh.heavy[x]] : kInfH;
     }
     // per-thread tables, lane-consecutive index s*B + t for position t*SM + s
     auto slot_of = [&](uint32_t p) { return (p % SM) * B + p / SM; };
@@ -504,16 +543,16 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge
         const uint32_t x = slot_of(p);
         bp.lrow[x] = light[p];
         bp.start[x] = hm.start[light[p]];
-        bp.bw[x] = bwp[p];
-        for (uint32_t a = 0; a < HA; ++a) bp.aw[(size_t)a * cap + x] = awp[order[a]][p];
-        uint8_t f = bex[p] ? 1 : 0;
-        if (HA >= 1 && aex[order[0]][p]) f |= 2;
-        if (HA >= 1 && p > 0 && heavy[order[0]] < light[p - 1]) f |= 4;
+        bp.bw[x] = sh.bw[p];
+        for (uint32_t a = 0; a < HA; ++a) bp.aw[(size_t)a * cap + x] = sh.aw[a][p];
+        uint8_t f = sh.bex[p] ? 1 : 0;
+        if (HA >= 1 && sh.aex[0][p]) f |= 2;
+        if (HA >= 1 && p > 0 && sh.heavy[0] < light[p - 1]) f |= 4;
         bp.pflags[x] = f;
         bp.ties_heavy = (p == 0 ? true : bp.ties_heavy) && (f & 2) && (!(f & 1) || (f & 4));
         bp.spos[light[p]] = (int32_t)p;
     }
-    for (size_t x = 0; x < order.size(); ++x) bp.spos[heavy[order[x]]] = -1 - (int32_t)x;
+    for (size_t x = 0; x < sh.heavy.size(); ++x) bp.spos[sh.heavy[x]] = -1 - (int32_t)x;
     // streamed-E chain kernel: [o][t][round_up(SM,4)]
     if (ge) {
         const uint32_t smp = (SM + 3) / 4 * 4;
@@ -587,6 +626,171 @@ void DeviceBandPlan::upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Pipelined chain plan (pipe.hip): chain-shaped models with exactly one heavy row F feeding the
+// light rows, F's heavy-row terms from itself only, and the other heavy row S (if any) feeding
+// no light row and not F.  Positions p (chain order) in blocks of 64*SM, one wave each.
+// ------------------------------------------------------------------------------------------
+PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm, uint32_t waves) {
+    PipePlan pp;
+    const uint32_t n = hm.n, S = hm.S;
+    if (S > 32) return pp;
+    const BandShape sh = analyze_band(hm);
+    if (!sh.ok || sh.HA != 1) return pp;
+    const uint32_t H = (uint32_t)sh.heavy.size();
+    float xff = kInfH, xss = kInfH, xsf = kInfH;
+    for (const auto& e : sh.exc[0]) {
+        if (e.first != 0) return pp;  // F <- S: F would depend on S, which depends on every light row
+        xff = e.second;
+    }
+    bool sx = false;
+    if (H == 2) {
+        for (const auto& e : sh.exc[1]) {
+            if (e.first == 1) xss = e.second;
+            else { xsf = e.second; sx = true; }
+        }
+    }
+    if (const char* e = std::getenv("SVH_PIPE_SM")) sm = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("SVH_PIPE_WAVES")) waves = (uint32_t)std::atoi(e);
+    // 2 slots per lane, 4 waves per workgroup: one wave per SIMD at the headline width (measured
+    // against 1 x 8, 1 x 4 and 2 x 8: DESIGN.md 5b)
+    if (sm == 0) sm = 2;
+    if (waves == 0) waves = 4;
+    if (!pipe_supported((int)sm, (int)waves, sx)) return pp;
+    const uint32_t nL = (uint32_t)sh.light.size();
+    const uint32_t bsz = 64 * sm;
+    pp.SM = sm;
+    pp.W = waves;
+    pp.nblk = (nL + bsz - 1) / bsz;
+    pp.G = (pp.nblk + waves - 1) / waves;
+    pp.P = pp.nblk * bsz;
+    pp.sx = sx;
+    pp.rowF = (int)sh.heavy[0];
+    pp.rowS = H == 2 ? (int)sh.heavy[1] : -1;
+    pp.startF = hm.start[sh.heavy[0]];
+    pp.startS = H == 2 ? hm.start[sh.heavy[1]] : kInfH;
+    const uint32_t P = pp.P;
+    pp.tab.assign((size_t)pp.nblk * S * sm * 64 * 2, kInfH);
+    pp.e0.assign((size_t)S * P, kInfH);
+    pp.start.assign(P, kInfH);
+    pp.lrow.assign(P, 0xFFFFFFFFu);
+    for (uint32_t p = 0; p < nL; ++p) {
+        const uint32_t j = sh.light[p], blk = p / bsz, lane = (p % bsz) / sm, s = p % sm;
+        pp.start[p] = hm.start[j];
+        pp.lrow[p] = j;
+        for (uint32_t o = 0; o < S; ++o) {
+            const float e = hm.emis[(size_t)o * n + j];
+            pp.e0[(size_t)o * P + p] = e;
+            float* t = pp.tab.data() + ((((size_t)blk * S + o) * sm + s) * 64 + lane) * 2;
+            t[0] = e + sh.bw[p];     // fl(E_o[p] + bw_p): the reference's first add of the chain term
+            t[1] = e + sh.aw[0][p];  // fl(E_o[p] + aw_p): ... of F's term
+        }
+    }
+    pp.hc.assign((size_t)S * 8, kInfH);
+    for (uint32_t o = 0; o < S; ++o) {
+        float* c = pp.hc.data() + (size_t)o * 8;
+        const float eF = hm.emis[(size_t)o * n + sh.heavy[0]];
+        const float eS = H == 2 ? hm.emis[(size_t)o * n + sh.heavy[1]] : kInfH;
+        c[0] = eS + (H == 2 ? sh.wh[1] : kInfH);  // A_S
+        c[1] = eF + sh.wh[0];  // A_F
+        c[2] = eS + xss;       // X_SS
+        c[3] = eF + xff;       // X_FF
+        c[4] = eS + xsf;       // X_SF
+        c[5] = eF;             // E_F (first observation)
+        c[6] = eS;             // E_S
+        c[7] = 0.0f;
+    }
+    pp.ok = true;
+    return pp;
+}
+
+void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream_t s) {
+    plan = p;
+    if (!p.ok) return;
+    d_tab.upload(p.tab.data(), p.tab.size() * 4, s);
+    d_e0.upload(p.e0.data(), p.e0.size() * 4, s);
+    d_start.upload(p.start.data(), p.start.size() * 4, s);
+    d_lrow.upload(p.lrow.data(), p.lrow.size() * 4, s);
+    d_hc.upload(p.hc.data(), p.hc.size() * 4, s);
+    d_fault.alloc(4);
+    hip_check(hipMemsetAsync(d_fault.ptr, 0, 4, s), "fault word");
+    std::memset(&view, 0, sizeof(view));
+    view.tab = d_tab.as<float2>();
+    view.e0 = d_e0.as<float>();
+    view.start = d_start.as<float>();
+    view.lrow = d_lrow.as<uint32_t>();
+    view.hc = d_hc.as<float>();
+    view.rowF = p.rowF;
+    view.rowS = p.rowS;
+    view.startF = p.startF;
+    view.startS = p.startS;
+    view.n = n;
+    view.S = S;
+    view.P = p.P;
+    view.nblk = p.nblk;
+    view.SM = p.SM;
+    view.W = p.W;
+    view.G = p.G;
+    view.sx = p.sx ? 1u : 0u;
+    view.fault = d_fault.as<uint32_t>();
+    if (const char* e = std::getenv("SVH_PIPE_DEBUG"); e && std::atoi(e)) {  // diagnostics only
+        d_stamps.alloc((size_t)65536 * kPipeStamps * 8);
+        hip_check(hipMemsetAsync(d_stamps.ptr, 0, d_stamps.bytes, s), "stamps");
+        view.stamps = d_stamps.as<unsigned long long>();
+    }
+}
+
+void DevicePipePlan::report_stamps(uint32_t nseq) const {
+    if (!view.stamps) return;
+    const size_t waves = (size_t)nseq * plan.G * plan.W;
+    if (waves > 65536 / kPipeStamps * kPipeStamps) return;
+    std::vector<unsigned long long> h(waves * kPipeStamps);
+    if (hipMemcpy(h.data(), view.stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    double sum[kPipeStamps] = {}, mx[kPipeStamps] = {};
+    for (size_t w = 0; w < waves; ++w)
+        for (int k = 0; k < kPipeStamps; ++k) {
+            sum[k] += (double)h[w * kPipeStamps + k];
+            mx[k] = std::max(mx[k], (double)h[w * kPipeStamps + k]);
+        }
+    std::fprintf(stderr, "pipe stamps (avg / max per wave): loop %.0f/%.0f head %.0f/%.0f tail %.0f/%.0f "
+                 "prev %.0f/%.0f next %.0f/%.0f gran %.0f/%.0f cons %.0f/%.0f iters %.0f\n",
+                 sum[0] / waves, mx[0], sum[1] / waves, mx[1], sum[2] / waves, mx[2], sum[3] / waves, mx[3],
+                 sum[4] / waves, mx[4], sum[5] / waves, mx[5], sum[6] / waves, mx[6], sum[7] / waves);
+    for (uint32_t g = 0; g < plan.G; ++g)
+        for (uint32_t w = 0; w < plan.W; ++w) {
+            const unsigned long long* r = h.data() + ((size_t)g * plan.W + w) * kPipeStamps;
+            std::fprintf(stderr, "  g%u w%u: loop %llu head %llu tail %llu prev %llu next %llu gran %llu cons %llu\n", g, w,
+                         r[0], r[1], r[2], r[3], r[4], r[5], r[6]);
+        }
+}
+
+void PipeScratchBuffers::ensure(uint32_t rows, uint32_t G, hipStream_t s) {
+    if (!d_ctr.ptr) {
+        d_ctr.alloc(16);
+        hip_check(hipMemsetAsync(d_ctr.ptr, 0, 16, s), "pipe counters");
+    }
+    if (view.ctr && rows <= view.rows && G <= view.G) return;
+    rows = std::max(rows, view.rows);
+    G = std::max(G, view.G);
+    auto zeroed = [&](DeviceBuffer& d, size_t bytes) {
+        d.alloc(bytes);
+        hip_check(hipMemsetAsync(d.ptr, 0, d.bytes, s), "pipe scratch");
+    };
+    zeroed(d_done, (size_t)rows * 4);
+    zeroed(d_part, (size_t)rows * G * 16);
+    zeroed(d_gran, (size_t)rows * std::max<uint32_t>(G - 1, 1) * kPipeGRing * 8);
+    zeroed(d_cons, (size_t)rows * G * 8);
+    zeroed(d_viol, (size_t)rows * 4);
+    view.ctr = d_ctr.as<uint32_t>();
+    view.done = d_done.as<uint32_t>();
+    view.part = d_part.as<uint64_t>();
+    view.gran = d_gran.as<uint64_t>();
+    view.cons = d_cons.as<uint32_t>();
+    view.viol = d_viol.as<uint32_t>();
+    view.rows = rows;
+    view.G = G;
+}
+
 void DeviceBandPlan::report_stamps(uint32_t nseq) const {
     if (!(view.dbg & (4u | 128u)) || !view.stamps) return;
     std::vector<unsigned long long> h((size_t)nseq * kMaxWaves * kBandStamps);
@@ -650,13 +854,23 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
     DeviceGuard g(device);
     hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
 
-    if (kernel_pref == SVH_KERNEL_AUTO || kernel_pref == SVH_KERNEL_BAND || kernel_pref == SVH_KERNEL_CHAIN) {
+    if (kernel_pref == SVH_KERNEL_AUTO || kernel_pref == SVH_KERNEL_BAND || kernel_pref == SVH_KERNEL_CHAIN ||
+        kernel_pref == SVH_KERNEL_PIPE) {
         BandPlan bpl;
         if (kernel_pref != SVH_KERNEL_BAND) bpl = make_band_plan(host, max_threads, true);
         if (!bpl.ok && kernel_pref != SVH_KERNEL_CHAIN) bpl = make_band_plan(host, max_threads, false);
         if (kernel_pref != SVH_KERNEL_AUTO && !bpl.ok)
             throw Error(SVH_E_UNSUPPORTED, "chain kernel requested but the model is not chain-shaped "
                                            "(or too large / too many symbols for it)");
+        // pipelined plan (its fallback is the chain / band plan above); SVH_PIPE=0 disables it
+        const char* pipe_env = std::getenv("SVH_PIPE");
+        if (bpl.ok && !(pipe_env && std::atoi(pipe_env) == 0)) {
+            const PipePlan ppl = make_pipe_plan(host);
+            if (ppl.ok) pipe.upload(ppl, host.n, host.S, stream);
+        }
+        if (kernel_pref == SVH_KERNEL_PIPE && !pipe.plan.ok)
+            throw Error(SVH_E_UNSUPPORTED, "pipelined kernel requested but the model does not qualify (chain shape "
+                                           "with one heavy row feeding the light rows, emit_num <= 32)");
         band.upload(bpl, host.n, host.S, stream);
         // wide batches: the 8-wave E-in-VGPR geometry holds one workgroup per CU; 4 waves with
         // streamed E fit two, which doubles throughput once every CU is busy
@@ -667,6 +881,12 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
         int cus = 0;
         hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device), "CU count");
         cu_count = (uint32_t)cus;
+        if (pipe.plan.ok) {
+            // AUTO: the pipelined plan while the batch holds at most two of its workgroups per CU
+            // (beyond that the chain kernel's higher throughput per CU wins); SVH_PIPE_MAX_NSEQ overrides
+            pipe_max_nseq = std::max<uint32_t>(1, 2 * cu_count / pipe.plan.G);
+            if (const char* e = std::getenv("SVH_PIPE_MAX_NSEQ")) pipe_max_nseq = (uint32_t)std::atoi(e);
+        }
     }
     Plan fast = make_plan(host, max_threads, true);
     fast_plan.upload(fast, stream);
@@ -725,11 +945,19 @@ CsrModel Model::csr_view() const {
 
 const DeviceBandPlan* Model::band_for(bool paths, uint32_t nseq) const {
     if (!band.plan.ok) return nullptr;
-    if (kernel_pref != SVH_KERNEL_AUTO && kernel_pref != SVH_KERNEL_BAND && kernel_pref != SVH_KERNEL_CHAIN)
+    if (kernel_pref != SVH_KERNEL_AUTO && kernel_pref != SVH_KERNEL_BAND && kernel_pref != SVH_KERNEL_CHAIN &&
+        kernel_pref != SVH_KERNEL_PIPE)  // PIPE: the chain plan is its fallback
         return nullptr;
     if (paths) return band.plan.paths_ok() ? &band : nullptr;  // decoded-path chain variant
     if (band_wide.plan.ok && nseq > cu_count) return &band_wide;
     return &band;
+}
+
+const DevicePipePlan* Model::pipe_for(uint32_t nseq) const {
+    if (!pipe.plan.ok) return nullptr;
+    if (kernel_pref == SVH_KERNEL_PIPE) return &pipe;
+    if (kernel_pref != SVH_KERNEL_AUTO || nseq > pipe_max_nseq) return nullptr;
+    return &pipe;
 }
 
 const DevicePlan* Model::plan_for(bool paths) const {
@@ -792,6 +1020,7 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
     const DevicePlan* p = plan_for(paths && steps);
     const DeviceBandPlan* bpl = band_for(paths && steps, nseq);
     i.kernel = bpl ? (bpl->plan.chain ? SVH_KERNEL_CHAIN : SVH_KERNEL_BAND) : p ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
+    const DevicePipePlan* ppl = !paths && steps && nseq ? pipe_for(nseq) : nullptr;
     i.family = p ? p->plan.family : -1;
     i.threads = p ? (int32_t)p->plan.B : (int32_t)std::min<uint32_t>(1024, round_up(host.n, 64));
     i.slots = p ? (int32_t)p->plan.SM : 0;
@@ -817,6 +1046,18 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
     i.wide_threads = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.B : 0;
     i.wide_slots = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.SM : 0;
     i.cu_count = cu_count;
+    if (ppl) {
+        i.kernel = SVH_KERNEL_PIPE;
+        i.threads = (int32_t)(64 * ppl->plan.W);
+        i.slots = (int32_t)ppl->plan.SM;
+        i.lds_bytes = pipe_lds_bytes(ppl->plan.W, host.S);
+    }
+    if (pipe.plan.ok) {
+        i.pipe_slots = (int32_t)pipe.plan.SM;
+        i.pipe_waves = (int32_t)pipe.plan.W;
+        i.pipe_groups = (int32_t)pipe.plan.G;
+        i.pipe_max_nseq = kernel_pref == SVH_KERNEL_PIPE ? 0xFFFFFFFFu : pipe_max_nseq;
+    }
     return i;
 }
 
@@ -963,6 +1204,12 @@ void Batch::run(uint32_t level, hipStream_t s) {
     } else if (paths) {
         fb.bp = d_bp.as<uint16_t>();
         fb.bp_off = d_bpoff.as<uint64_t>();
+    }
+    pipe_ran = false;
+    if (!paths && model->pipe_for(nseq)) {  // pipelined plan: scratch for this batch's rows
+        pipe.ensure(nseq, model->pipe.plan.G, s);
+        fb.pipe = &pipe.view;
+        pipe_ran = model->band_for(false, nseq) != nullptr;  // launch_steps' condition
     }
     auto launch_step_kernel = [&](const FusedBatch& b, bool want_paths) { model->launch_steps(b, want_paths, s); };
 
@@ -1259,6 +1506,22 @@ void Batch::read_async(hipStream_t s, float* scores, int64_t* best, int32_t* pat
 void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) const {
     const DevicePlan* dp = plan_for(want_paths);
     const DeviceBandPlan* bpl = band_for(want_paths, b.nseq);
+    const DevicePipePlan* ppl = want_paths ? nullptr : pipe_for(b.nseq);
+    if (ppl && bpl && b.pipe && b.pipe->rows >= b.nseq && b.pipe->G >= ppl->plan.G) {
+        hip_check(launch_pipe(ppl->view, b, *b.pipe, s), "pipelined Viterbi kernel");
+        if (ppl->view.stamps) {
+            hip_check(hipStreamSynchronize(s), "stamps");
+            ppl->report_stamps(b.nseq);
+        }
+        // rows whose speculation failed run again on the serial chain kernel (the others exit)
+        FusedBatch fb = b;
+        fb.run_mask = b.pipe->viol;
+        fb.pipe = nullptr;
+        const int ha = (int)std::max<uint32_t>(bpl->plan.HA, 1);
+        if (bpl->plan.chain) hip_check(launch_chain(bpl->view, ha, fb, s), "chain Viterbi kernel (pipe fallback)");
+        else hip_check(launch_band(bpl->view, ha, fb, s), "band Viterbi kernel (pipe fallback)");
+        return;
+    }
     if (bpl) {
         const int ha = (int)std::max<uint32_t>(bpl->plan.HA, 1);
         if (bpl->plan.chain) hip_check(launch_chain(bpl->view, ha, b, s), "chain Viterbi kernel");
@@ -1276,6 +1539,14 @@ void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) co
 }
 
 void Model::check_fault() const {
+    if (pipe.plan.ok && pipe.view.fault) {
+        uint32_t fault = 0;
+        hip_check(hipMemcpy(&fault, pipe.view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
+        if (fault) {
+            hip_check(hipMemset(pipe.view.fault, 0, 4), "fault reset");
+            throw Error(SVH_E_HIP, "pipelined kernel: a bounded wait gave up (results invalid)");
+        }
+    }
     for (const DeviceBandPlan* p : {&band, &band_wide}) {
         if (!p->plan.ok || !p->view.fault) continue;
         uint32_t fault = 0;
@@ -1286,6 +1557,18 @@ void Model::check_fault() const {
             throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
         }
     }
+}
+
+uint64_t Batch::pipe_fallbacks() {
+    DeviceGuard g(model->device);
+    if (!ran) throw Error(SVH_E_STATE, "no run recorded");
+    if (!pipe_ran) return 0;
+    hip_check(hipEventSynchronize(ev_stop), "hipEventSynchronize");
+    std::vector<uint32_t> v(nseq);
+    hip_check(hipMemcpy(v.data(), pipe.view.viol, (size_t)nseq * 4, hipMemcpyDeviceToHost), "fallback flags D2H");
+    uint64_t c = 0;
+    for (uint32_t x : v) c += x != 0;
+    return c;
 }
 
 float Batch::elapsed_ms() {

@@ -124,6 +124,38 @@ struct DeviceBandPlan {
     void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_BAND_DEBUG & 4)
 };
 
+// Host tables of the pipelined chain kernel (pipe.hip); ok == false when the model does not
+// qualify (kernels.h, PipeModel).
+struct PipePlan {
+    bool ok = false;
+    bool sx = false;
+    uint32_t SM = 0, W = 0, G = 0, nblk = 0, P = 0;
+    int rowF = -1, rowS = -1;
+    float startF = 0, startS = 0;
+    std::vector<float> tab;     // [nblk][S][SM][64][2]
+    std::vector<float> e0;      // [S][P]
+    std::vector<float> start;   // [P]
+    std::vector<uint32_t> lrow; // [P]
+    std::vector<float> hc;      // [S][8]
+};
+// sm = 0 / waves = 0: defaults (SVH_PIPE_SM / SVH_PIPE_WAVES override them, diagnostics)
+PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm = 0, uint32_t waves = 0);
+
+struct DevicePipePlan {
+    PipePlan plan;
+    DeviceBuffer d_tab, d_e0, d_start, d_lrow, d_hc, d_fault, d_stamps;
+    PipeModel view{};
+    void upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream_t s);
+    void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_PIPE_DEBUG): first sequence's waves
+};
+
+// Scratch of the pipelined kernel, owned by a batch (grow-only).
+struct PipeScratchBuffers {
+    DeviceBuffer d_ctr, d_done, d_part, d_gran, d_cons, d_viol;
+    PipeScratch view{};
+    void ensure(uint32_t rows, uint32_t G, hipStream_t s);
+};
+
 struct Model {
     std::mutex mu;
     int device = 0;
@@ -134,6 +166,8 @@ struct Model {
     DeviceBandPlan band_wide;        // chain plan for batches wider than the chip: streamed E,
                                      // 4 waves (more workgroups per CU), scores only
     uint32_t cu_count = 0;
+    DevicePipePlan pipe;             // pipelined chain plan (latency path for small batches)
+    uint32_t pipe_max_nseq = 0;      // AUTO: pipelined plan for batches of at most this many rows
     DevicePlan fast_plan;            // fastest fused plan (may use uniform heavy rows)
     DevicePlan paths_plan_storage;   // term-by-term plan when fast_plan is uniform
     const DevicePlan* paths_plan = nullptr;
@@ -150,6 +184,8 @@ struct Model {
     const DevicePlan* plan_for(bool paths) const;
     // Chain plan to run for a pass over nseq sequences (nullptr: use plan_for(paths)).
     const DeviceBandPlan* band_for(bool paths, uint32_t nseq = 0) const;
+    // Pipelined plan for a scores-only pass over nseq rows (nullptr: none).
+    const DevicePipePlan* pipe_for(uint32_t nseq) const;
     void spec_build(uint32_t level, hipStream_t s);
     svh_model_info info(uint32_t nseq = 0, bool paths = false, uint32_t level = 0) const;
     // throws if a chain-kernel bounded wait gave up since the model was created (synchronous)
@@ -169,6 +205,7 @@ struct Batch {
     DeviceBuffer d_bp, d_bpoff, d_pathoff, d_paths;
     bool chain_paths = false;  // paths from the chain kernel's compact records (else fused / generic)
     DeviceBuffer d_cmask, d_cmaskoff, d_hrec, d_hrecoff, d_ckpt, d_ckptoff;
+    PipeScratchBuffers pipe;  // pipelined kernel scratch (sized for the rows of each launch)
     // _spec runs
     DeviceBuffer d_vbuf, d_nchunks, d_tbegin, d_vrow;
     uint32_t spec_ready_level = 0;
@@ -189,6 +226,9 @@ struct Batch {
     void run(uint32_t level, hipStream_t s);
     void read(hipStream_t s, float* scores, int64_t* best, int32_t* paths);
     float elapsed_ms();
+    // rows of the last run that the pipelined kernel handed to the serial kernel (synchronous)
+    uint64_t pipe_fallbacks();
+    bool pipe_ran = false;  // the last run used the pipelined kernel
     // opt-in time-parallel scores (segments of >= seg observations, probes of `probe`; see
     // runtime.cpp); synchronous; *fallbacks = segments that did not converge within the probe
     void run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream_t s, uint64_t* fallbacks);

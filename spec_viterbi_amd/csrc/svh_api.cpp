@@ -256,6 +256,13 @@ int svh_batch_elapsed_ms(svh_batch_t b, float* ms) {
     });
 }
 
+int svh_batch_fallbacks(svh_batch_t b, uint64_t* rows) {
+    return guarded([&] {
+        require(b && rows, "null argument");
+        *rows = b->impl->pipe_fallbacks();
+    });
+}
+
 int svh_batch_plan(svh_batch_t b, uint32_t level, svh_model_info* info) {
     return guarded([&] {
         require(b && info, "null argument");

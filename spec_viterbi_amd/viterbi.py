@@ -138,6 +138,13 @@ class DeviceBatch:
         _lib.check(_lib.lib.svh_batch_plan(self._h, int(level), ctypes.byref(i)))
         return {name: getattr(i, name) for name, _ in i._fields_}
 
+    def fallbacks(self) -> int:
+        """Rows of the last run that the pipelined kernel re-ran on the serial chain kernel
+        (svh_batch_fallbacks; 0 if the last run did not use the pipelined kernel)."""
+        r = ctypes.c_uint64()
+        _lib.check(_lib.lib.svh_batch_fallbacks(self._h, ctypes.byref(r)))
+        return int(r.value)
+
     def elapsed_ms(self) -> float:
         ms = ctypes.c_float()
         _lib.check(_lib.lib.svh_batch_elapsed_ms(self._h, ctypes.byref(ms)))

@@ -1,0 +1,192 @@
+"""GPU parity of the pipelined chain kernel (pipe.hip, SVH_KERNEL_PIPE).
+
+The kernel speculates that the feeder row N never takes its light-state term and checks that
+exactly at every observation; a failing sequence is re-run by the serial chain kernel, so results
+are bit-identical either way.  Because that fallback would also hide a wrong pipelined result,
+every reference workload here asserts that no row fell back (`DeviceBatch.fallbacks() == 0`), and
+random models whose N does take its light term assert that rows did fall back and still match.
+"""
+import numpy as np
+import pytest
+
+import spec_viterbi_amd as svh
+from spec_viterbi_amd import _lib
+from oracle import oracle
+from tests.conftest import chmm, ess
+from tests.helpers import bit_equal, first_mismatch, from_hex, load_golden, random_chain_hmm, random_seqs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    assert _lib.device_count() > 0, "no HIP device visible (GPU tests must run on an MI355X)"
+
+
+def run(hmm, seqs, kernel=_lib.SVH_KERNEL_PIPE, level=0):
+    model = svh.DeviceModel(hmm, kernel=kernel)
+    if level >= 2:
+        model.spec_build(level)
+    b = model.batch(seqs)
+    b.run(level)
+    s, best = b.read()
+    plan = b.plan(level)
+    return s, best, (b.fallbacks() if kernel == _lib.SVH_KERNEL_PIPE else 0), plan
+
+
+def assert_same(s1, b1, s2, b2):
+    for q in range(len(s1)):
+        assert bit_equal(s1[q], s2[q]), (q, first_mismatch(s1[q], s2[q]))
+    assert np.array_equal(b1, b2)
+
+
+def oracle_check(hmm, seqs, scores, best):
+    refs, _ = oracle.viterbi_batch(hmm, seqs)
+    for q, seq in enumerate(seqs):
+        ref = refs[q]
+        assert bit_equal(scores[q], ref), (q, first_mismatch(scores[q], ref))
+        ref_best = int(np.argmin(ref)) if np.isfinite(ref).any() else 0
+        assert best[q] == ref_best, (q, best[q], ref_best)
+
+
+def test_pipe_headline_goldens_no_fallback():
+    """BASELINE config 3 (2405.chmm x emit_50_3500_20, all 50 sequences) on the pipelined kernel:
+    the committed golden rows bit-exact, the whole batch equal to the serial chain kernel, and no
+    row fell back."""
+    g = load_golden("chmm2405_emit50")
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
+    s, b, fb, plan = run(hmm, seqs)
+    assert plan["kernel"] == _lib.SVH_KERNEL_PIPE
+    assert fb == 0
+    for rec in g["sequences"]:
+        q = rec["index"]
+        assert bit_equal(s[q], from_hex(rec["scores"])), first_mismatch(s[q], from_hex(rec["scores"]))
+        assert b[q] == rec["best_state"]
+    sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
+    assert_same(s, b, sc, bc)
+
+
+def test_pipe_auto_selects_pipe_for_small_batches():
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    model = svh.DeviceModel(hmm)
+    info = model.info()
+    assert info["pipe_slots"] > 0 and info["pipe_groups"] > 1
+    small = model.batch(random_seqs(20, [50] * 4, seed=1))
+    assert small.plan()["kernel"] == _lib.SVH_KERNEL_PIPE
+    wide = model.batch(random_seqs(20, [8] * (info["pipe_max_nseq"] + 1), seed=2))
+    assert wide.plan()["kernel"] == _lib.SVH_KERNEL_CHAIN
+
+
+@pytest.mark.parametrize("name", ["100.chmm", "500.chmm", "1001.chmm", "1509.chmm", "2050.chmm"])
+def test_pipe_reference_models_vs_oracle(name):
+    hmm = svh.read_HMM(chmm(name))
+    seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    s, b, fb, _ = run(hmm, seqs)
+    assert fb == 0
+    oracle_check(hmm, seqs[:1], s[:1], b[:1])
+    sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
+    assert_same(s, b, sc, bc)
+
+
+def test_pipe_covid_ragged_no_fallback():
+    """BASELINE config 5's workload: 16 real protein sequences of 38..7096 observations."""
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("covid-19.ess"))
+    s, b, fb, _ = run(hmm, seqs)
+    assert fb == 0
+    sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
+    assert_same(s, b, sc, bc)
+    short = [q for q in range(len(seqs)) if len(seqs[q]) < 400]
+    oracle_check(hmm, [seqs[q] for q in short], s[short], b[short])
+
+
+@pytest.mark.parametrize("L", [1, 2, 3, 31, 32, 33, 63, 64, 65, 95, 1023, 1024, 1025, 1057, 2049])
+def test_pipe_sequence_lengths(L):
+    """Head (single observations up to a multiple of 32), body (groups of 8) and tail; symbol
+    windows of 1024; three workgroups per sequence (L = 700 light states)."""
+    hmm = random_chain_hmm(700, S=20, seed=L, n_from_m=False)
+    seqs = random_seqs(20, [L, L + 5, max(1, L - 3)], seed=L)
+    s, b, fb, plan = run(hmm, seqs)
+    assert plan["pipe_groups"] >= 2 and fb == 0
+    oracle_check(hmm, seqs, s, b)
+
+
+def test_pipe_long_sequence_many_ring_laps():
+    """A 60,000-observation sequence: the granule ring (256 slots) turns ~230 times, 59 symbol
+    windows, five workgroups of one sequence in flight."""
+    hmm = random_chain_hmm(2400, S=20, seed=3, n_from_m=False)
+    seqs = random_seqs(20, [60000, 4000], seed=4)
+    s, b, fb, plan = run(hmm, seqs)
+    assert fb == 0 and plan["pipe_groups"] >= 4
+    sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
+    assert_same(s, b, sc, bc)
+
+
+def test_pipe_fallback_rows_match_oracle():
+    """Models whose feeder row takes its light term (cheap M -> N): the speculation fails, those
+    rows are re-run serially, and every score still matches the oracle."""
+    total_fb = 0
+    for seed in range(6):
+        hmm = random_chain_hmm(300, S=8, seed=seed)
+        # make M_j -> N nearly free so N's light term wins somewhere
+        rows, cols = hmm.trans_rows.astype(np.int64), hmm.trans_cols.astype(np.int64)
+        probs = hmm.trans_probs.copy()
+        probs[(cols == 0) & (rows != 0)] = np.float32(0.0)
+        hmm.trans_probs = probs
+        seqs = random_seqs(8, [700, 1, 40, 333], seed=seed)
+        s, b, fb, _ = run(hmm, seqs)
+        total_fb += fb
+        oracle_check(hmm, seqs, s, b)
+    assert total_fb > 0
+
+
+@pytest.mark.parametrize("variant", [dict(self_n=False), dict(c_from_m=False), dict(self_c=False),
+                                     dict(gap=37), dict(zero_emis=0.2), dict(ties=True), dict(inf_edges=0.1),
+                                     dict(start=(0, 5, 301))])
+def test_pipe_chain_variants(variant):
+    hmm = random_chain_hmm(600, S=12, seed=11, **variant)
+    seqs = random_seqs(12, [300, 64, 1, 97], seed=12)
+    s, b, fb, _ = run(hmm, seqs)
+    oracle_check(hmm, seqs, s, b)
+
+
+@pytest.mark.parametrize("geom", [(1, 4), (1, 8), (2, 4), (2, 8)])
+def test_pipe_geometries(geom, monkeypatch):
+    monkeypatch.setenv("SVH_PIPE_SM", str(geom[0]))
+    monkeypatch.setenv("SVH_PIPE_WAVES", str(geom[1]))
+    hmm = random_chain_hmm(1300, S=20, seed=21, n_from_m=False)
+    seqs = random_seqs(20, [500, 129, 2], seed=22)
+    s, b, fb, plan = run(hmm, seqs)
+    assert (plan["slots"], plan["pipe_waves"]) == geom
+    assert fb == 0
+    oracle_check(hmm, seqs, s, b)
+
+
+def test_pipe_spec_level2_tail():
+    """_spec level 2: the chunks run on the dense products, the tail on the pipelined kernel from
+    device scores (begin > 0, v_in); bit-exact against the oracle's level-2 association."""
+    hmm = svh.read_HMM(chmm("100.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    seqs = [seqs[0][:301], seqs[1][:64], seqs[2][:2]]
+    s, b, fb, plan = run(hmm, seqs, level=2)
+    for q, seq in enumerate(seqs):
+        ref = oracle.viterbi_spec(hmm, 2, seq)
+        assert bit_equal(s[q], ref), (q, first_mismatch(s[q], ref))
+
+
+def test_pipe_reruns_and_two_batches_share_nothing_stale():
+    """Launch epochs: re-running a batch, and a second batch of different lengths on the same
+    model, never read another launch's boundary granules."""
+    hmm = random_chain_hmm(900, S=20, seed=31, n_from_m=False)
+    model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_PIPE)
+    a = model.batch(random_seqs(20, [900, 33], seed=32))
+    bb = model.batch(random_seqs(20, [100, 2000, 5], seed=33))
+    res = []
+    for batch in (a, bb, a, bb, a):
+        batch.run()
+        res.append(batch.read())
+        assert batch.fallbacks() == 0
+    for i, j in ((0, 2), (2, 4), (1, 3)):
+        assert_same(res[i][0], res[i][1], res[j][0], res[j][1])
+    oracle_check(hmm, random_seqs(20, [900, 33], seed=32), res[0][0], res[0][1])
