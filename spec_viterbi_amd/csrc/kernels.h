@@ -194,6 +194,8 @@ struct PipeModel {
     uint32_t sx;            // S has a term from F
     uint32_t* fault;        // set non-zero if a bounded wait gave up
     unsigned long long* stamps;  // diagnostics (SVH_PIPE_DEBUG): [ticket][W][8] counters, or null
+    uint32_t diag;               // diagnostics with stamps (SVH_PIPE_DEBUG bits > 1): 1 = no boundary
+                                 // exchange (every wave runs as block 0; timing only, wrong results)
 };
 constexpr int kPipeStamps = 8;
 // Per-batch scratch of the pipelined kernel (sized for `rows` rows).

@@ -396,8 +396,11 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 // observations): the previous group's (lane 7 feeds the first step) and, SRC 1,
                 // the next group's, read one group ahead whenever the producer is far enough
                 float bv_prev = bprev;  // lane 7 (all lanes) = boundary of t-1
+                // SRC 1: the next group's vector, loaded at the end of every group (stale unless
+                // next_ok) into this one loop-carried register, re-loaded there when it was stale
                 float bv_next = kInf;
                 bool next_ok = false;
+                if constexpr (SRC == 1) bv_next = ring_prev[(lane & 7u) * 64 + 63];  // group at t (t % 32 == 0)
                 for (; t + 32 <= len; t += 32) {
                     if (dbg) ++dg[7];
                     window_for(t);
@@ -414,15 +417,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         constexpr uint32_t j = decltype(jc)::value;
                         const uint32_t tg = t + 8 * j;
                         float bv = kInf;  // lanes 0..7: the previous block's last scores of tg..tg+7
-                        if constexpr (SRC == 1) {
-                            if (next_ok) {
-                                bv = bv_next;
-                            } else {
-                                wait_prev(tg + 8);
-                                asm volatile("" ::: "memory");
-                                bv = ring_prev[(8 * j + (lane & 7u)) * 64 + 63];
-                            }
-                        } else if constexpr (SRC == 2) {
+                        if constexpr (SRC == 2) {
                             asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // gq[j]: 3 later loads in flight
                             uint64_t gv = gq[j];
                             while (__builtin_amdgcn_ballot_w64((uint32_t)(gv >> 32) != gtag(ep, tg)) != 0) {
@@ -440,6 +435,14 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         auto one = [&](auto kc) {
                             constexpr uint32_t k = decltype(kc)::value;
                             const uint32_t o = (uint32_t)((sw >> (8 * k)) & 0xFFu);
+                            if constexpr (SRC == 1 && k == 1) {  // step 0 used only the previous vector
+                                if (!next_ok) {  // the producer had not published this group: wait, re-load
+                                    wait_prev(tg + 8);
+                                    asm volatile("" ::: "memory");
+                                    bv_next = ring_prev[(8 * j + (lane & 7u)) * 64 + 63];
+                                }
+                            }
+                            if constexpr (SRC == 1) bv = bv_next;
                             if constexpr (k == 0) {
                                 step(o, [&](float& xb, float& xa, float eb, float ea, float f, float xl) {
                                     chain_terms_v<7>(xb, xa, eb, ea, bv_prev, f, xl);
@@ -450,7 +453,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                 });
                             }
                             ring_w[(8 * j + k) * 64 + lane] = v[SM - 1];
-                            if constexpr (k == 5) {  // the counts checked at the end of the group
+                            if constexpr (k == 4) {  // the counts checked at the end of the group
                                 asm volatile("" ::: "memory");
                                 if constexpr (SRC == 1) pc_rd = lds_ld32(cnt_w - 1);
                                 if constexpr (DST == 1) nc_rd = lds_ld32(cnt_w + 1);
@@ -467,9 +470,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         bv_prev = bv;
                         asm volatile("" ::: "memory");
                         lds_put1(cnt_addr, tg + 8);
-                        if constexpr (SRC == 1) {  // the next group's boundary vector, if published
+                        if constexpr (SRC == 1) {  // the next group's boundary vector (valid if next_ok)
                             next_ok = (uint32_t)uniform((int)pc_rd) >= tg + 16;
-                            if (next_ok) bv_next = ring_prev[(((8 * j + 8) & (kR - 1)) + (lane & 7u)) * 64 + 63];
+                            asm volatile("" ::: "memory");
+                            bv_next = ring_prev[(((8 * j + 8) & (kR - 1)) + (lane & 7u)) * 64 + 63];
                         }
                         if constexpr (DST == 2) {
                             // granules of the previous group (read back from the ring one group ago)
@@ -506,7 +510,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             if (dbg) dg[2] = __builtin_amdgcn_s_memtime() - c0;
         };
 
-        if (len > first) {
+        if (len > first && dbg && (m.diag & 1u)) {
+            sweep(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});  // no exchange (timing only)
+        } else if (len > first) {
             using I0 = std::integral_constant<int, 0>;
             using I1 = std::integral_constant<int, 1>;
             using I2 = std::integral_constant<int, 2>;

@@ -737,6 +737,7 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
         d_stamps.alloc((size_t)65536 * kPipeStamps * 8);
         hip_check(hipMemsetAsync(d_stamps.ptr, 0, d_stamps.bytes, s), "stamps");
         view.stamps = d_stamps.as<unsigned long long>();
+        view.diag = (uint32_t)std::atoi(e) >> 1;
     }
 }
 
