@@ -1021,7 +1021,8 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
     const DevicePlan* p = plan_for(paths && steps);
     const DeviceBandPlan* bpl = band_for(paths && steps, nseq);
     i.kernel = bpl ? (bpl->plan.chain ? SVH_KERNEL_CHAIN : SVH_KERNEL_BAND) : p ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
-    const DevicePipePlan* ppl = !paths && steps && nseq ? pipe_for(nseq) : nullptr;
+    // the pipelined plan runs scores-only passes and the step-kernel tail of _spec level >= 2
+    const DevicePipePlan* ppl = !paths && nseq ? pipe_for(nseq) : nullptr;
     i.family = p ? p->plan.family : -1;
     i.threads = p ? (int32_t)p->plan.B : (int32_t)std::min<uint32_t>(1024, round_up(host.n, 64));
     i.slots = p ? (int32_t)p->plan.SM : 0;
