@@ -71,12 +71,15 @@ void svh_ess_free(svh_ess_t e);
  * is chain-shaped with at most one heavy row feeding the light rows (every reference .chmm), else
  * the fused (or generic) kernel with 16-bit backpointers. */
 enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2, SVH_KERNEL_BAND = 3,
-       SVH_KERNEL_CHAIN = 4, SVH_KERNEL_PIPE = 5 };
+       SVH_KERNEL_CHAIN = 4, SVH_KERNEL_PIPE = 5, SVH_KERNEL_PIPE_WIDE = 6 };
 /* PIPE: the pipelined chain kernel (MSV-shaped models whose feeder row N takes terms only from
  * the light rows and itself): a sequence's states are split over many waves and CUs; N's light
  * term is speculated away and checked exactly at every observation, and a sequence that fails
  * the check is re-run by the serial chain kernel (same results either way).  AUTO uses it for
- * scores-only passes over batches too small to fill the chip with the chain kernel. */
+ * scores-only passes over batches too small to fill the chip with the chain kernel.
+ * PIPE_WIDE: the same recurrence with one block of states per workgroup and one sequence per wave
+ * (the block's table in LDS, shared by the waves): the throughput plan AUTO uses for wider
+ * batches. */
 
 typedef struct {
     int32_t device;      /* HIP device ordinal; -1 = the caller's current device */
@@ -117,6 +120,10 @@ typedef struct {
     int32_t pipe_waves;    /* ... waves per workgroup */
     int32_t pipe_groups;   /* ... workgroups per sequence */
     uint32_t pipe_max_nseq; /* AUTO runs the pipelined plan for batches of at most this many sequences */
+    int32_t pipew_slots;   /* wide pipelined plan (SVH_KERNEL_PIPE_WIDE): states per lane, 0 = none */
+    int32_t pipew_waves;   /* ... sequences (waves) per workgroup */
+    int32_t pipew_blocks;  /* ... workgroups per sequence */
+    uint32_t pipew_min_nseq; /* AUTO runs it for batches of at least this many sequences */
 } svh_model_info;
 /* The model's plan for a one-sequence scores-only run (kernel/threads/slots describe it). */
 int svh_model_get_info(svh_model_t m, svh_model_info* info);

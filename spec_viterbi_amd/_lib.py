@@ -31,6 +31,7 @@ SVH_KERNEL_GENERIC = 2
 SVH_KERNEL_BAND = 3
 SVH_KERNEL_CHAIN = 4
 SVH_KERNEL_PIPE = 5
+SVH_KERNEL_PIPE_WIDE = 6
 SVH_BATCH_PATHS = 1
 
 
@@ -54,6 +55,7 @@ class svh_model_info(ctypes.Structure):
         ("spec_level", c_uint64), ("spec_bytes", c_uint64), ("paths_kernel", c_int32), ("wide_threads", c_int32),
         ("wide_slots", c_int32), ("cu_count", c_uint32), ("pipe_slots", c_int32), ("pipe_waves", c_int32),
         ("pipe_groups", c_int32), ("pipe_max_nseq", c_uint32),
+        ("pipew_slots", c_int32), ("pipew_waves", c_int32), ("pipew_blocks", c_int32), ("pipew_min_nseq", c_uint32),
     ]
 
 

@@ -214,6 +214,16 @@ inline size_t pipe_lds_bytes(uint32_t W, uint32_t S) {
 }
 bool pipe_supported(int sm, int waves, bool sx);
 hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
+// Wide pipelined plan (pipe_wide.hip): one block of 64*SM positions per workgroup, W sequences
+// (one per wave), the block's table [nblk][S][NC][64] float4 in LDS (PipeModel.tab; G = nblk);
+// NC = SM/2 (eb|ea) chunks + {A_S A_F X_SS X_FF} [+ {X_SF 0 0 0} when sx], constants per lane.
+inline uint32_t pipew_chunks(uint32_t SM, bool sx) { return SM / 2 + 1 + (sx ? 1 : 0); }
+inline size_t pipew_lds_bytes(uint32_t SM, uint32_t W, uint32_t S, bool sx) {
+    // table [S][NC][64] float4 | boundary ring [W][8][64] | ticket
+    return (size_t)S * pipew_chunks(SM, sx) * 64 * 16 + (size_t)W * 8 * 64 * 4 + 16;
+}
+bool pipew_supported(int sm, int waves, bool sx);
+hipError_t launch_pipew(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
 
 // CSR of T^T used by the generic kernel and the _spec precompute.
 struct CsrModel {

@@ -27,12 +27,12 @@
 // fl(a + .) is monotone), F' = fl(X_FF + F), and the check fl(A_F + m) < F' (a violation: F
 // would have taken its light term, the speculation and everything after it is void).
 // The last workgroup of a sequence to finish combines the partials (S, argmin, violation).
-#include "device_common.h"
-#include "kernels.h"
+#include "pipe_common.h"
 
 namespace svh {
 
 using namespace dev;
+using namespace pipe_dev;
 
 namespace {
 
@@ -40,20 +40,6 @@ typedef float f32x32 __attribute__((ext_vector_type(32)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr uint32_t kR = kPipeRing;
-constexpr uint32_t kGR = kPipeGRing;
-constexpr uint32_t kSpinLimit = 1u << 22;
-constexpr uint32_t kNoRow = 0xFFFFFFFFu;
-
-__device__ __forceinline__ uint32_t lds_ld32(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Agent-scope relaxed accesses: global_load / global_store ... sc1 (L2-coherent, bypass L1).
-__device__ __forceinline__ uint64_t g_ld64(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void g_st64(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // One lane's LDS store of a wave-uniform word: EXEC narrowed to lane 0 inside the asm (no
 // divergent branch in the compiler's view).
@@ -101,26 +87,6 @@ __device__ __forceinline__ void chain_terms_v(float& xb, float& xa, float eb, fl
             : "=&v"(xb), "=&v"(xa)
             : "v"(bvv), "v"(eb), "v"(f), "v"(ea), "v"(x), "n"(16 - R));  // lane 0 <- lane R
     }
-}
-
-__device__ __forceinline__ float readlane_f(float x, uint32_t l) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), (int)l));
-}
-__device__ __forceinline__ uint32_t readlane_u(uint32_t x, uint32_t l) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
-}
-
-// Granule tag of observation s in this launch: epoch and ring lap (a slot is rewritten every
-// kGR observations; flow control keeps the consumer within one lap).
-__device__ __forceinline__ uint32_t gtag(uint32_t ep, uint32_t s) {
-    return ((ep % 0xFFFFFu + 1u) << 12) | ((s >> 8) & 0xFFFu);  // never 0 (zeroed memory)
-}
-static_assert(kGR == 256, "gtag assumes a 256-slot ring");
-
-// Granule prefetch into a register the loop carries (tied operand: no copy at the back edge, so
-// no wait is forced there); the caller waits with an explicit vmcnt before reading it.
-__device__ __forceinline__ void g_prefetch64(uint64_t& dst, const uint64_t* p) {
-    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "+v"(dst) : "v"(p) : "memory");
 }
 
 template <int SM, int W, bool SX>

@@ -631,7 +631,7 @@ void DeviceBandPlan::upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream
 // light rows, F's heavy-row terms from itself only, and the other heavy row S (if any) feeding
 // no light row and not F.  Positions p (chain order) in blocks of 64*SM, one wave each.
 // ------------------------------------------------------------------------------------------
-PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm, uint32_t waves) {
+PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm, uint32_t waves, bool wide) {
     PipePlan pp;
     const uint32_t n = hm.n, S = hm.S;
     if (S > 32) return pp;
@@ -650,19 +650,22 @@ PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm, uint32_t waves) {
             else { xsf = e.second; sx = true; }
         }
     }
-    if (const char* e = std::getenv("SVH_PIPE_SM")) sm = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("SVH_PIPE_WAVES")) waves = (uint32_t)std::atoi(e);
-    // 2 slots per lane, 4 waves per workgroup: one wave per SIMD at the headline width (measured
-    // against 1 x 8, 1 x 4 and 2 x 8: DESIGN.md 5b)
-    if (sm == 0) sm = 2;
-    if (waves == 0) waves = 4;
-    if (!pipe_supported((int)sm, (int)waves, sx)) return pp;
+    if (const char* e = std::getenv(wide ? "SVH_PIPEW_SM" : "SVH_PIPE_SM")) sm = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv(wide ? "SVH_PIPEW_WAVES" : "SVH_PIPE_WAVES")) waves = (uint32_t)std::atoi(e);
+    // latency plan: 2 slots per lane, 4 waves per workgroup: one wave per SIMD at the headline
+    // width (measured against 1 x 8, 1 x 4 and 2 x 8: DESIGN.md 5b); wide plan: 8 slots per
+    // lane, 16 sequences per workgroup
+    if (sm == 0) sm = wide ? 8 : 2;
+    if (waves == 0) waves = wide ? 16 : 4;
+    if (wide ? !pipew_supported((int)sm, (int)waves, sx) : !pipe_supported((int)sm, (int)waves, sx)) return pp;
+    if (wide && pipew_lds_bytes(sm, waves, S, sx) > 160 * 1024) return pp;
     const uint32_t nL = (uint32_t)sh.light.size();
     const uint32_t bsz = 64 * sm;
+    pp.wide = wide;
     pp.SM = sm;
     pp.W = waves;
     pp.nblk = (nL + bsz - 1) / bsz;
-    pp.G = (pp.nblk + waves - 1) / waves;
+    pp.G = wide ? pp.nblk : (pp.nblk + waves - 1) / waves;
     pp.P = pp.nblk * bsz;
     pp.sx = sx;
     pp.rowF = (int)sh.heavy[0];
@@ -670,7 +673,8 @@ PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm, uint32_t waves) {
     pp.startF = hm.start[sh.heavy[0]];
     pp.startS = H == 2 ? hm.start[sh.heavy[1]] : kInfH;
     const uint32_t P = pp.P;
-    pp.tab.assign((size_t)pp.nblk * S * sm * 64 * 2, kInfH);
+    const uint32_t nc = wide ? pipew_chunks(sm, sx) : 0;  // wide: 16-byte chunks per symbol and lane
+    pp.tab.assign(wide ? (size_t)pp.nblk * S * nc * 64 * 4 : (size_t)pp.nblk * S * sm * 64 * 2, kInfH);
     pp.e0.assign((size_t)S * P, kInfH);
     pp.start.assign(P, kInfH);
     pp.lrow.assign(P, 0xFFFFFFFFu);
@@ -681,12 +685,34 @@ PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm, uint32_t waves) {
         for (uint32_t o = 0; o < S; ++o) {
             const float e = hm.emis[(size_t)o * n + j];
             pp.e0[(size_t)o * P + p] = e;
-            float* t = pp.tab.data() + ((((size_t)blk * S + o) * sm + s) * 64 + lane) * 2;
-            t[0] = e + sh.bw[p];     // fl(E_o[p] + bw_p): the reference's first add of the chain term
-            t[1] = e + sh.aw[0][p];  // fl(E_o[p] + aw_p): ... of F's term
+            const float eb = e + sh.bw[p];     // fl(E_o[p] + bw_p): the reference's first add of the chain term
+            const float ea = e + sh.aw[0][p];  // fl(E_o[p] + aw_p): ... of F's term
+            if (wide) {
+                // chunks of 4 per lane: [eb_1 .. eb_{SM-1}, eb_0] then [ea_0 .. ea_{SM-1}]
+                const uint32_t ib = s == 0 ? sm - 1 : s - 1, ia = sm + s;
+                float* base = pp.tab.data() + (((size_t)blk * S + o) * nc) * 64 * 4;
+                base[((ib / 4) * 64 + lane) * 4 + ib % 4] = eb;
+                base[((ia / 4) * 64 + lane) * 4 + ia % 4] = ea;
+            } else {
+                float* t = pp.tab.data() + ((((size_t)blk * S + o) * sm + s) * 64 + lane) * 2;
+                t[0] = eb;
+                t[1] = ea;
+            }
         }
     }
     pp.hc.assign((size_t)S * 8, kInfH);
+    auto wide_consts = [&](uint32_t o, const float* c) {  // wide: constants chunk(s) of every lane
+        for (uint32_t blk = 0; blk < pp.nblk; ++blk)
+            for (uint32_t lane = 0; lane < 64; ++lane) {
+                float* base = pp.tab.data() + ((((size_t)blk * S + o) * nc + sm / 2) * 64 + lane) * 4;
+                for (int k = 0; k < 4; ++k) base[k] = c[k];
+                if (sx) {
+                    float* b2 = base + 64 * 4;
+                    b2[0] = c[4];
+                    b2[1] = b2[2] = b2[3] = 0.0f;
+                }
+            }
+    };
     for (uint32_t o = 0; o < S; ++o) {
         float* c = pp.hc.data() + (size_t)o * 8;
         const float eF = hm.emis[(size_t)o * n + sh.heavy[0]];
@@ -699,6 +725,7 @@ PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm, uint32_t waves) {
         c[5] = eF;             // E_F (first observation)
         c[6] = eS;             // E_S
         c[7] = 0.0f;
+        if (wide) wide_consts(o, c);
     }
     pp.ok = true;
     return pp;
@@ -856,7 +883,7 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
     hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
 
     if (kernel_pref == SVH_KERNEL_AUTO || kernel_pref == SVH_KERNEL_BAND || kernel_pref == SVH_KERNEL_CHAIN ||
-        kernel_pref == SVH_KERNEL_PIPE) {
+        kernel_pref == SVH_KERNEL_PIPE || kernel_pref == SVH_KERNEL_PIPE_WIDE) {
         BandPlan bpl;
         if (kernel_pref != SVH_KERNEL_BAND) bpl = make_band_plan(host, max_threads, true);
         if (!bpl.ok && kernel_pref != SVH_KERNEL_CHAIN) bpl = make_band_plan(host, max_threads, false);
@@ -869,7 +896,11 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
             const PipePlan ppl = make_pipe_plan(host);
             if (ppl.ok) pipe.upload(ppl, host.n, host.S, stream);
         }
-        if (kernel_pref == SVH_KERNEL_PIPE && !pipe.plan.ok)
+        if (bpl.ok && pipe.plan.ok && !(std::getenv("SVH_PIPEW") && std::atoi(std::getenv("SVH_PIPEW")) == 0)) {
+            const PipePlan wpl = make_pipe_plan(host, 0, 0, true);
+            if (wpl.ok) pipe_wide.upload(wpl, host.n, host.S, stream);
+        }
+        if ((kernel_pref == SVH_KERNEL_PIPE && !pipe.plan.ok) || (kernel_pref == SVH_KERNEL_PIPE_WIDE && !pipe_wide.plan.ok))
             throw Error(SVH_E_UNSUPPORTED, "pipelined kernel requested but the model does not qualify (chain shape "
                                            "with one heavy row feeding the light rows, emit_num <= 32)");
         band.upload(bpl, host.n, host.S, stream);
@@ -887,6 +918,11 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
             // (beyond that the chain kernel's higher throughput per CU wins); SVH_PIPE_MAX_NSEQ overrides
             pipe_max_nseq = std::max<uint32_t>(1, 2 * cu_count / pipe.plan.G);
             if (const char* e = std::getenv("SVH_PIPE_MAX_NSEQ")) pipe_max_nseq = (uint32_t)std::atoi(e);
+        }
+        if (pipe_wide.plan.ok) {
+            // AUTO: the wide pipelined plan for batches beyond the latency plan's range
+            pipew_min_nseq = pipe_max_nseq + 1;
+            if (const char* e = std::getenv("SVH_PIPEW_MIN_NSEQ")) pipew_min_nseq = (uint32_t)std::atoi(e);
         }
     }
     Plan fast = make_plan(host, max_threads, true);
@@ -947,7 +983,7 @@ CsrModel Model::csr_view() const {
 const DeviceBandPlan* Model::band_for(bool paths, uint32_t nseq) const {
     if (!band.plan.ok) return nullptr;
     if (kernel_pref != SVH_KERNEL_AUTO && kernel_pref != SVH_KERNEL_BAND && kernel_pref != SVH_KERNEL_CHAIN &&
-        kernel_pref != SVH_KERNEL_PIPE)  // PIPE: the chain plan is its fallback
+        kernel_pref != SVH_KERNEL_PIPE && kernel_pref != SVH_KERNEL_PIPE_WIDE)  // PIPE*: the chain plan is its fallback
         return nullptr;
     if (paths) return band.plan.paths_ok() ? &band : nullptr;  // decoded-path chain variant
     if (band_wide.plan.ok && nseq > cu_count) return &band_wide;
@@ -955,10 +991,12 @@ const DeviceBandPlan* Model::band_for(bool paths, uint32_t nseq) const {
 }
 
 const DevicePipePlan* Model::pipe_for(uint32_t nseq) const {
-    if (!pipe.plan.ok) return nullptr;
-    if (kernel_pref == SVH_KERNEL_PIPE) return &pipe;
-    if (kernel_pref != SVH_KERNEL_AUTO || nseq > pipe_max_nseq) return nullptr;
-    return &pipe;
+    if (kernel_pref == SVH_KERNEL_PIPE) return pipe.plan.ok ? &pipe : nullptr;
+    if (kernel_pref == SVH_KERNEL_PIPE_WIDE) return pipe_wide.plan.ok ? &pipe_wide : nullptr;
+    if (kernel_pref != SVH_KERNEL_AUTO) return nullptr;
+    if (pipe.plan.ok && nseq <= pipe_max_nseq) return &pipe;
+    if (pipe_wide.plan.ok && nseq >= pipew_min_nseq) return &pipe_wide;
+    return nullptr;
 }
 
 const DevicePlan* Model::plan_for(bool paths) const {
@@ -1049,10 +1087,19 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
     i.wide_slots = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.SM : 0;
     i.cu_count = cu_count;
     if (ppl) {
-        i.kernel = SVH_KERNEL_PIPE;
+        i.kernel = ppl->plan.wide ? SVH_KERNEL_PIPE_WIDE : SVH_KERNEL_PIPE;
         i.threads = (int32_t)(64 * ppl->plan.W);
         i.slots = (int32_t)ppl->plan.SM;
-        i.lds_bytes = pipe_lds_bytes(ppl->plan.W, host.S);
+        i.lds_bytes = ppl->plan.wide ? pipew_lds_bytes(ppl->plan.SM, ppl->plan.W, host.S, ppl->plan.sx)
+                                     : pipe_lds_bytes(ppl->plan.W, host.S);
+    }
+    if (pipe_wide.plan.ok) {
+        i.pipew_slots = (int32_t)pipe_wide.plan.SM;
+        i.pipew_waves = (int32_t)pipe_wide.plan.W;
+        i.pipew_blocks = (int32_t)pipe_wide.plan.G;
+        i.pipew_min_nseq = kernel_pref == SVH_KERNEL_PIPE_WIDE ? 0u
+                           : kernel_pref == SVH_KERNEL_AUTO    ? pipew_min_nseq
+                                                               : 0xFFFFFFFFu;
     }
     if (pipe.plan.ok) {
         i.pipe_slots = (int32_t)pipe.plan.SM;
@@ -1208,8 +1255,8 @@ void Batch::run(uint32_t level, hipStream_t s) {
         fb.bp_off = d_bpoff.as<uint64_t>();
     }
     pipe_ran = false;
-    if (!paths && model->pipe_for(nseq)) {  // pipelined plan: scratch for this batch's rows
-        pipe.ensure(nseq, model->pipe.plan.G, s);
+    if (const DevicePipePlan* pp = paths ? nullptr : model->pipe_for(nseq)) {  // pipelined plan: scratch
+        pipe.ensure(nseq, pp->plan.G, s);
         fb.pipe = &pipe.view;
         pipe_ran = model->band_for(false, nseq) != nullptr;  // launch_steps' condition
     }
@@ -1510,8 +1557,9 @@ void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) co
     const DeviceBandPlan* bpl = band_for(want_paths, b.nseq);
     const DevicePipePlan* ppl = want_paths ? nullptr : pipe_for(b.nseq);
     if (ppl && bpl && b.pipe && b.pipe->rows >= b.nseq && b.pipe->G >= ppl->plan.G) {
-        hip_check(launch_pipe(ppl->view, b, *b.pipe, s), "pipelined Viterbi kernel");
-        if (ppl->view.stamps) {
+        if (ppl->plan.wide) hip_check(launch_pipew(ppl->view, b, *b.pipe, s), "wide pipelined Viterbi kernel");
+        else hip_check(launch_pipe(ppl->view, b, *b.pipe, s), "pipelined Viterbi kernel");
+        if (ppl->view.stamps && !ppl->plan.wide) {
             hip_check(hipStreamSynchronize(s), "stamps");
             ppl->report_stamps(b.nseq);
         }
@@ -1541,11 +1589,12 @@ void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) co
 }
 
 void Model::check_fault() const {
-    if (pipe.plan.ok && pipe.view.fault) {
+    for (const DevicePipePlan* p : {&pipe, &pipe_wide}) {
+        if (!p->plan.ok || !p->view.fault) continue;
         uint32_t fault = 0;
-        hip_check(hipMemcpy(&fault, pipe.view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
+        hip_check(hipMemcpy(&fault, p->view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
         if (fault) {
-            hip_check(hipMemset(pipe.view.fault, 0, 4), "fault reset");
+            hip_check(hipMemset(p->view.fault, 0, 4), "fault reset");
             throw Error(SVH_E_HIP, "pipelined kernel: a bounded wait gave up (results invalid)");
         }
     }

@@ -137,9 +137,10 @@ struct PipePlan {
     std::vector<float> start;   // [P]
     std::vector<uint32_t> lrow; // [P]
     std::vector<float> hc;      // [S][8]
+    bool wide = false;          // pipe_wide.hip layout: tab [nblk][S][SM/2][64][4], W sequences per workgroup
 };
 // sm = 0 / waves = 0: defaults (SVH_PIPE_SM / SVH_PIPE_WAVES override them, diagnostics)
-PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm = 0, uint32_t waves = 0);
+PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm = 0, uint32_t waves = 0, bool wide = false);
 
 struct DevicePipePlan {
     PipePlan plan;
@@ -168,6 +169,8 @@ struct Model {
     uint32_t cu_count = 0;
     DevicePipePlan pipe;             // pipelined chain plan (latency path for small batches)
     uint32_t pipe_max_nseq = 0;      // AUTO: pipelined plan for batches of at most this many rows
+    DevicePipePlan pipe_wide;        // wide pipelined plan (throughput path for batches that fill the chip)
+    uint32_t pipew_min_nseq = 0;     // AUTO: wide pipelined plan for batches of at least this many rows
     DevicePlan fast_plan;            // fastest fused plan (may use uniform heavy rows)
     DevicePlan paths_plan_storage;   // term-by-term plan when fast_plan is uniform
     const DevicePlan* paths_plan = nullptr;

@@ -330,11 +330,11 @@ def test_run_sharded_cli_covid_paths(tmp_path):
 
 def test_wide_batch_streamed_plan_2405():
     """A batch with more sequences than CUs runs the wide chain plan (4 waves, streamed E, two
-    workgroups per CU): bit-exact against the oracle, and against the same sequences run in
-    batches narrow enough for the default plan; its lengths cover 1, the 8-observation group
-    edges and the symbol-chunk refill."""
+    workgroups per CU; forced: AUTO runs the wide pipelined plan there): bit-exact against the
+    oracle, and against the same sequences run in batches narrow enough for the default plan; its
+    lengths cover 1, the 8-observation group edges and the symbol-chunk refill."""
     hmm = svh.read_HMM(chmm("2405.chmm"))
-    model = svh.DeviceModel(hmm)
+    model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_CHAIN)
     info = model.info()
     assert info["kernel"] == _lib.SVH_KERNEL_CHAIN and info["wide_threads"] == 256, info
     rng = np.random.default_rng(11)
@@ -388,11 +388,11 @@ def test_hip_impl_cache_follows_the_hmm_passed():
 
 @pytest.mark.parametrize("name", ["1301.chmm", "1509.chmm", "1901.chmm", "2365.chmm"])
 def test_wide_plan_other_pfam_models(name):
-    """The wide chain plan (picked for batches of more sequences than CUs) on other eligible Pfam
-    models: every sequence equal to narrow batches of the same sequences, a sample bit-exact
-    against the oracle; svh_batch_plan names the plan each batch runs."""
+    """The wide chain plan (the chain kernel's plan for batches of more sequences than CUs) on
+    other eligible Pfam models: every sequence equal to narrow batches of the same sequences, a
+    sample bit-exact against the oracle; svh_batch_plan names the plan each batch runs."""
     hmm = svh.read_HMM(chmm(name))
-    model = svh.DeviceModel(hmm)
+    model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_CHAIN)
     info = model.info()
     if not info["wide_threads"]:
         pytest.skip(f"{name}: no wide plan ({info['threads']} threads narrow)")
@@ -404,12 +404,9 @@ def test_wide_plan_other_pfam_models(name):
     assert plan["threads"] == info["wide_threads"] and plan["slots"] == info["wide_slots"], plan
     batch.run()
     wide, wide_best = batch.read()
-    small = model.batch(seqs[:100])  # narrow batches: the pipelined plan while it fits, else the 8-wave chain
+    small = model.batch(seqs[:100])  # narrow batches: the 8-wave chain plan
     sp = small.plan()
-    if 100 <= info["pipe_max_nseq"]:
-        assert sp["kernel"] == _lib.SVH_KERNEL_PIPE and sp["slots"] == info["pipe_slots"], sp
-    else:
-        assert sp["threads"] == info["threads"], sp
+    assert sp["kernel"] == _lib.SVH_KERNEL_CHAIN and sp["threads"] == info["threads"], sp
     narrow = np.concatenate([model.viterbi(seqs[k:k + 100])[0] for k in range(0, len(seqs), 100)])
     assert bit_equal(wide, narrow)
     for q in [0, 1, 2, 3, 150, len(seqs) - 1]:

@@ -1,4 +1,6 @@
-"""GPU parity of the pipelined chain kernel (pipe.hip, SVH_KERNEL_PIPE).
+"""GPU parity of the pipelined chain kernels: the latency plan (pipe.hip, SVH_KERNEL_PIPE) and the
+wide throughput plan (pipe_wide.hip, SVH_KERNEL_PIPE_WIDE: one position block per workgroup, one
+sequence per wave); most tests run on both.
 
 The kernel speculates that the feeder row N never takes its light-state term and checks that
 exactly at every observation; a failing sequence is re-run by the serial chain kernel, so results
@@ -16,6 +18,8 @@ from tests.conftest import chmm, ess
 from tests.helpers import bit_equal, first_mismatch, from_hex, load_golden, random_chain_hmm, random_seqs
 
 pytestmark = pytest.mark.gpu
+PIPES = [_lib.SVH_KERNEL_PIPE, _lib.SVH_KERNEL_PIPE_WIDE]
+pipes = pytest.mark.parametrize("kern", PIPES, ids=["pipe", "pipew"])
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -31,7 +35,7 @@ def run(hmm, seqs, kernel=_lib.SVH_KERNEL_PIPE, level=0):
     b.run(level)
     s, best = b.read()
     plan = b.plan(level)
-    return s, best, (b.fallbacks() if kernel == _lib.SVH_KERNEL_PIPE else 0), plan
+    return s, best, (b.fallbacks() if kernel in PIPES else 0), plan
 
 
 def assert_same(s1, b1, s2, b2):
@@ -49,15 +53,16 @@ def oracle_check(hmm, seqs, scores, best):
         assert best[q] == ref_best, (q, best[q], ref_best)
 
 
-def test_pipe_headline_goldens_no_fallback():
+@pipes
+def test_pipe_headline_goldens_no_fallback(kern):
     """BASELINE config 3 (2405.chmm x emit_50_3500_20, all 50 sequences) on the pipelined kernel:
     the committed golden rows bit-exact, the whole batch equal to the serial chain kernel, and no
     row fell back."""
     g = load_golden("chmm2405_emit50")
     hmm = svh.read_HMM(chmm("2405.chmm"))
     seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
-    s, b, fb, plan = run(hmm, seqs)
-    assert plan["kernel"] == _lib.SVH_KERNEL_PIPE
+    s, b, fb, plan = run(hmm, seqs, kernel=kern)
+    assert plan["kernel"] == kern
     assert fb == 0
     for rec in g["sequences"]:
         q = rec["index"]
@@ -75,25 +80,33 @@ def test_pipe_auto_selects_pipe_for_small_batches():
     small = model.batch(random_seqs(20, [50] * 4, seed=1))
     assert small.plan()["kernel"] == _lib.SVH_KERNEL_PIPE
     wide = model.batch(random_seqs(20, [8] * (info["pipe_max_nseq"] + 1), seed=2))
-    assert wide.plan()["kernel"] == _lib.SVH_KERNEL_CHAIN
+    assert info["pipew_min_nseq"] == info["pipe_max_nseq"] + 1 and info["pipew_blocks"] == 5, info
+    assert wide.plan()["kernel"] == _lib.SVH_KERNEL_PIPE_WIDE
+    assert wide.plan()["threads"] == 64 * info["pipew_waves"] and wide.plan()["slots"] == info["pipew_slots"]
+    # the chain kernel forced: its wide plan
+    chain = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_CHAIN).batch(random_seqs(20, [8] * 300, seed=3))
+    assert chain.plan()["kernel"] == _lib.SVH_KERNEL_CHAIN
 
 
+@pipes
 @pytest.mark.parametrize("name", ["100.chmm", "500.chmm", "1001.chmm", "1509.chmm", "2050.chmm"])
-def test_pipe_reference_models_vs_oracle(name):
+def test_pipe_reference_models_vs_oracle(name, kern):
     hmm = svh.read_HMM(chmm(name))
     seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
-    s, b, fb, _ = run(hmm, seqs)
+    s, b, fb, _ = run(hmm, seqs, kernel=kern)
     assert fb == 0
     oracle_check(hmm, seqs[:1], s[:1], b[:1])
     sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
     assert_same(s, b, sc, bc)
 
 
-def test_pipe_covid_ragged_no_fallback():
-    """BASELINE config 5's workload: 16 real protein sequences of 38..7096 observations."""
+@pipes
+def test_pipe_covid_ragged_no_fallback(kern):
+    """BASELINE config 5's workload: 16 real protein sequences of 38..7096 observations (the wide
+    plan: 16 ragged sequences in one workgroup per block)."""
     hmm = svh.read_HMM(chmm("2405.chmm"))
     seqs = svh.read_emit_seq(ess("covid-19.ess"))
-    s, b, fb, _ = run(hmm, seqs)
+    s, b, fb, _ = run(hmm, seqs, kernel=kern)
     assert fb == 0
     sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
     assert_same(s, b, sc, bc)
@@ -101,29 +114,33 @@ def test_pipe_covid_ragged_no_fallback():
     oracle_check(hmm, [seqs[q] for q in short], s[short], b[short])
 
 
+@pipes
 @pytest.mark.parametrize("L", [1, 2, 3, 31, 32, 33, 63, 64, 65, 95, 1023, 1024, 1025, 1057, 2049])
-def test_pipe_sequence_lengths(L):
+def test_pipe_sequence_lengths(L, kern):
     """Head (single observations up to a multiple of 32), body (groups of 8) and tail; symbol
-    windows of 1024; three workgroups per sequence (L = 700 light states)."""
-    hmm = random_chain_hmm(700, S=20, seed=L, n_from_m=False)
+    windows of 1024; three workgroups per sequence (latency plan, L = 700 light states) or
+    three position blocks (wide plan, L = 1300)."""
+    hmm = random_chain_hmm(700 if kern == _lib.SVH_KERNEL_PIPE else 1300, S=20, seed=L, n_from_m=False)
     seqs = random_seqs(20, [L, L + 5, max(1, L - 3)], seed=L)
-    s, b, fb, plan = run(hmm, seqs)
-    assert plan["pipe_groups"] >= 2 and fb == 0
+    s, b, fb, plan = run(hmm, seqs, kernel=kern)
+    assert (plan["pipe_groups"] if kern == _lib.SVH_KERNEL_PIPE else plan["pipew_blocks"]) >= 2 and fb == 0
     oracle_check(hmm, seqs, s, b)
 
 
-def test_pipe_long_sequence_many_ring_laps():
+@pipes
+def test_pipe_long_sequence_many_ring_laps(kern):
     """A 60,000-observation sequence: the granule ring (256 slots) turns ~230 times, 59 symbol
     windows, five workgroups of one sequence in flight."""
     hmm = random_chain_hmm(2400, S=20, seed=3, n_from_m=False)
     seqs = random_seqs(20, [60000, 4000], seed=4)
-    s, b, fb, plan = run(hmm, seqs)
-    assert fb == 0 and plan["pipe_groups"] >= 4
+    s, b, fb, plan = run(hmm, seqs, kernel=kern)
+    assert fb == 0 and (plan["pipe_groups"] if kern == _lib.SVH_KERNEL_PIPE else plan["pipew_blocks"]) >= 4
     sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
     assert_same(s, b, sc, bc)
 
 
-def test_pipe_fallback_rows_match_oracle():
+@pipes
+def test_pipe_fallback_rows_match_oracle(kern):
     """Models whose feeder row takes its light term (cheap M -> N): the speculation fails, those
     rows are re-run serially, and every score still matches the oracle."""
     total_fb = 0
@@ -135,7 +152,7 @@ def test_pipe_fallback_rows_match_oracle():
         probs[(cols == 0) & (rows != 0)] = np.float32(0.0)
         hmm.trans_probs = probs
         seqs = random_seqs(8, [700, 1, 40, 333], seed=seed)
-        s, b, fb, _ = run(hmm, seqs)
+        s, b, fb, _ = run(hmm, seqs, kernel=kern)
         total_fb += fb
         oracle_check(hmm, seqs, s, b)
     assert total_fb > 0
@@ -144,10 +161,22 @@ def test_pipe_fallback_rows_match_oracle():
 @pytest.mark.parametrize("variant", [dict(self_n=False), dict(c_from_m=False), dict(self_c=False),
                                      dict(gap=37), dict(zero_emis=0.2), dict(ties=True), dict(inf_edges=0.1),
                                      dict(start=(0, 5, 301))])
-def test_pipe_chain_variants(variant):
+@pipes
+def test_pipe_chain_variants(variant, kern):
     hmm = random_chain_hmm(600, S=12, seed=11, **variant)
     seqs = random_seqs(12, [300, 64, 1, 97], seed=12)
-    s, b, fb, _ = run(hmm, seqs)
+    s, b, fb, _ = run(hmm, seqs, kernel=kern)
+    oracle_check(hmm, seqs, s, b)
+
+
+@pytest.mark.parametrize("waves", [8, 12, 16])
+def test_pipew_geometries(waves, monkeypatch):
+    """Wide plan with 8, 12 and 16 sequences per workgroup: ragged batch wider than one workgroup."""
+    monkeypatch.setenv("SVH_PIPEW_WAVES", str(waves))
+    hmm = random_chain_hmm(1300, S=20, seed=23, n_from_m=False)
+    seqs = random_seqs(20, [500, 129, 2, 64, 1030] * 5, seed=24)
+    s, b, fb, plan = run(hmm, seqs, kernel=_lib.SVH_KERNEL_PIPE_WIDE)
+    assert plan["pipew_waves"] == waves and plan["threads"] == 64 * waves and fb == 0
     oracle_check(hmm, seqs, s, b)
 
 
@@ -163,23 +192,25 @@ def test_pipe_geometries(geom, monkeypatch):
     oracle_check(hmm, seqs, s, b)
 
 
-def test_pipe_spec_level2_tail():
+@pipes
+def test_pipe_spec_level2_tail(kern):
     """_spec level 2: the chunks run on the dense products, the tail on the pipelined kernel from
     device scores (begin > 0, v_in); bit-exact against the oracle's level-2 association."""
     hmm = svh.read_HMM(chmm("100.chmm"))
     seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
     seqs = [seqs[0][:301], seqs[1][:64], seqs[2][:2]]
-    s, b, fb, plan = run(hmm, seqs, level=2)
+    s, b, fb, plan = run(hmm, seqs, kernel=kern, level=2)
     for q, seq in enumerate(seqs):
         ref = oracle.viterbi_spec(hmm, 2, seq)
         assert bit_equal(s[q], ref), (q, first_mismatch(s[q], ref))
 
 
-def test_pipe_reruns_and_two_batches_share_nothing_stale():
+@pipes
+def test_pipe_reruns_and_two_batches_share_nothing_stale(kern):
     """Launch epochs: re-running a batch, and a second batch of different lengths on the same
     model, never read another launch's boundary granules."""
     hmm = random_chain_hmm(900, S=20, seed=31, n_from_m=False)
-    model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_PIPE)
+    model = svh.DeviceModel(hmm, kernel=kern)
     a = model.batch(random_seqs(20, [900, 33], seed=32))
     bb = model.batch(random_seqs(20, [100, 2000, 5], seed=33))
     res = []
@@ -190,3 +221,35 @@ def test_pipe_reruns_and_two_batches_share_nothing_stale():
     for i, j in ((0, 2), (2, 4), (1, 3)):
         assert_same(res[i][0], res[i][1], res[j][0], res[j][1])
     oracle_check(hmm, random_seqs(20, [900, 33], seed=32), res[0][0], res[0][1])
+
+
+def test_pipew_wide_batch_equals_chain_and_oracle():
+    """AUTO on a batch wider than the latency plan's range: the wide pipelined plan, every row equal
+    to the chain kernel's wide plan, a sample bit-exact against the oracle (random symbols: rows
+    whose speculation fails fall back, still exact)."""
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    model = svh.DeviceModel(hmm)
+    rng = np.random.default_rng(17)
+    lens = [1, 2, 31, 32, 33, 257, 1025] + list(rng.integers(1, 400, size=model.info()["pipew_min_nseq"] + 60))
+    seqs = [rng.integers(0, hmm.emit_num, size=int(k)).astype(np.uint64) for k in lens]
+    batch = model.batch(seqs)
+    assert batch.plan()["kernel"] == _lib.SVH_KERNEL_PIPE_WIDE
+    batch.run()
+    s, b = batch.read()
+    sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
+    assert_same(s, b, sc, bc)
+    sample = [0, 1, 2, 3, 4, 5, 6, 100, len(seqs) - 1]
+    oracle_check(hmm, [seqs[q] for q in sample], s[sample], b[sample])
+
+
+@pytest.mark.parametrize("name", ["1301.chmm", "1901.chmm", "2365.chmm"])
+def test_pipew_other_pfam_models_replicated(name):
+    """Other Pfam models, the reference's emit_50 sequences replicated past the latency plan's
+    range with synthetic copies (as bench.py --replicate): equal to the chain kernel."""
+    hmm = svh.read_HMM(chmm(name))
+    base = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
+    rng = np.random.default_rng(9)
+    seqs = list(base) + [rng.integers(0, hmm.emit_num, size=len(x) // 4 + 1).astype(np.uint64) for x in base] * 3
+    s, b, fb, plan = run(hmm, seqs, kernel=_lib.SVH_KERNEL_PIPE_WIDE)
+    sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
+    assert_same(s, b, sc, bc)

@@ -52,7 +52,9 @@ def main():
         times.append(batch.elapsed_ms())
     scores, _ = batch.read()
     ok = None
-    if a.model == "2405.chmm" and a.ess == "emit_50_3500_20.ess" and a.level <= 2:
+    # (diagnostic ablations, SVH_*_DEBUG, give wrong results by design: not checked)
+    diag = any(os.environ.get(k) for k in ("SVH_PIPE_DEBUG", "SVH_BAND_DEBUG"))
+    if a.model == "2405.chmm" and a.ess == "emit_50_3500_20.ess" and a.level <= 2 and not diag:
         from tests.helpers import bit_equal, from_hex, load_golden
 
         g = load_golden("chmm2405_emit50")

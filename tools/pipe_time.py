@@ -1,5 +1,7 @@
-"""Median kernel time of the pipelined plan (geometry from SVH_PIPE_SM / SVH_PIPE_WAVES) and a
-bit-exact comparison with the serial chain kernel.  python tools/pipe_time.py MODEL ESS [REPS]"""
+"""Median kernel time of the pipelined plans (latency geometry from SVH_PIPE_SM / SVH_PIPE_WAVES,
+wide geometry from SVH_PIPEW_SM / SVH_PIPEW_WAVES) against the serial chain kernel (its wide plan
+for batches of more sequences than CUs), with a bit-exact comparison.
+python tools/pipe_time.py MODEL ESS [REPS] [REPLICATE] [KERNELS]   KERNELS: e.g. chain,pipe,pipew"""
 import os
 import sys
 
@@ -15,12 +17,15 @@ h = read_HMM(os.path.join(root, "chmm_files", sys.argv[1] + ".chmm"))
 seqs = read_emit_seq(os.path.join(root, "ess_files", sys.argv[2] + ".ess"))
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
 rep = int(sys.argv[4]) if len(sys.argv) > 4 else 1  # copies of the file's sequences (synthetic)
+names = (sys.argv[5] if len(sys.argv) > 5 else "chain,pipe").split(",")
 if rep > 1:
     rng = np.random.default_rng(7)
     seqs = list(seqs) + [rng.integers(0, h.emit_num, size=len(s)).astype(np.uint64) for _ in range(rep - 1) for s in seqs]
+kernels = {"chain": _lib.SVH_KERNEL_CHAIN, "pipe": _lib.SVH_KERNEL_PIPE, "pipew": _lib.SVH_KERNEL_PIPE_WIDE,
+           "auto": _lib.SVH_KERNEL_AUTO}
 res = {}
-for name, k in (("chain", _lib.SVH_KERNEL_CHAIN), ("pipe", _lib.SVH_KERNEL_PIPE)):
-    m = DeviceModel(h, kernel=k)
+for name in names:
+    m = DeviceModel(h, kernel=kernels[name])
     b = m.batch(seqs)
     b.run()
     ts = []
@@ -28,9 +33,17 @@ for name, k in (("chain", _lib.SVH_KERNEL_CHAIN), ("pipe", _lib.SVH_KERNEL_PIPE)
         b.run()
         ts.append(b.elapsed_ms())
     s, bb = b.read()
-    res[name] = (np.where(s == 0, 0, s), bb, float(np.median(ts)), b.plan())
-eq = np.array_equal(res["chain"][0], res["pipe"][0]) and np.array_equal(res["chain"][1], res["pipe"][1])
-p = res["pipe"][3]
-print(f"{sys.argv[1]} x {sys.argv[2]} x{rep} SM={p['slots']} W={p['pipe_waves']} G={p['pipe_groups']}: "
-      f"chain {res['chain'][2]:.3f} ms pipe {res['pipe'][2]:.3f} ms equal={eq}", flush=True)
-sys.exit(0 if eq else 1)
+    fb = b.fallbacks()
+    res[name] = (np.where(s == 0, 0, s), bb, float(np.median(ts)), b.plan(), fb)
+ref = res[names[0]]
+ok = True
+line = f"{sys.argv[1]} x {sys.argv[2]} x{rep} ({len(seqs)} seqs):"
+for name in names:
+    r = res[name]
+    eq = np.array_equal(ref[0], r[0]) and np.array_equal(ref[1], r[1])
+    ok &= eq
+    p = r[3]
+    line += (f" {name} {r[2]:.3f} ms [k{p['kernel']} {p['threads']}x{p['slots']} fb={r[4]}]"
+             + ("" if eq else " DIFFERS"))
+print(line, flush=True)
+sys.exit(0 if ok else 1)

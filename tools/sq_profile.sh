@@ -2,7 +2,7 @@
 # rocprofv3 evidence for the chain kernel's roofline (run on the GPU box via gpurun):
 # per workload, one --kernel-trace --stats pass, two SQ counter passes (VALU issue, wait split)
 # and separate FETCH_SIZE / WRITE_SIZE passes; tools/sq_summary.py reduces them to JSON.
-#   TAG=r02 WORKLOADS="narrow wide" tools/sq_profile.sh
+#   TAG=r02 WORKLOADS="narrow wide" tools/sq_profile.sh   (SQ3=1: an LDS counter pass as well)
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -26,6 +26,7 @@ for w in ${WORKLOADS:-narrow wide}; do
     run $w trace --kernel-trace --stats -- $ARGS &&
     run $w sq1 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -- $ARGS &&
     run $w sq2 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS -- $ARGS &&
+    { [ -z "$SQ3" ] || run $w sq3 --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL -- $ARGS; } &&
     run $w fetch --pmc FETCH_SIZE -- $ARGS &&
     run $w write --pmc WRITE_SIZE -- $ARGS || { echo "workload $w failed"; exit 1; }
     python3 tools/sq_summary.py "$OUT/$w" > "$OUT/$w/summary.json" && cat "$OUT/$w/summary.json"
