@@ -40,7 +40,7 @@ DATA = os.path.join(ROOT, "data")
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_GHZ = 2.4         # MI355X_MICROARCH.md: max shader clock
-KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain", 5: "pipe"}
+KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain", 5: "pipe", 6: "pipew"}
 
 
 def parse(argv=None):
@@ -247,14 +247,19 @@ def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc) -> dict:
     cycle.  Peak = the SIMDs the launch occupies x that rate x 2.4 GHz; achieved = SQ_INSTS_VALU
     per launch / HIP-event kernel time.  The pipelined kernel runs nseq x pipe_groups workgroups
     of pipe_waves waves; `issue_frac_all` also counts its SALU and LDS instructions, which take a
-    wave's issue slot the same way (its bound at one wave per SIMD)."""
+    wave's issue slot the same way (its bound at one wave per SIMD).  The wide pipelined kernel runs
+    ceil(nseq / W) x pipew_blocks workgroups of W waves (threads / 64), one per CU (its LDS)."""
     waves_per_wg = max(1, int(plan["threads"]) // 64)
     pipe = plan["kernel"] == 5
     wide = plan["threads"] == info.get("wide_threads") and plan["slots"] == info.get("wide_slots") and nseq > info["cu_count"]
     wg_per_cu = 4 if wide else 1  # launch-bounds occupancy of the wide plan; one WG per CU otherwise
+    pipew = plan["kernel"] == 6
     wgs = nseq * int(info.get("pipe_groups", 1)) if pipe else nseq
     if pipe:
         wg_per_cu = max(1, -(-wgs // max(info["cu_count"], 1)))
+    if pipew:
+        wgs = -(-nseq // waves_per_wg) * int(info.get("pipew_blocks", 1))
+        wg_per_cu = 1
     cus = min(info["cu_count"], -(-wgs // wg_per_cu)) if info["cu_count"] else 256
     waves_per_simd = min(8, waves_per_wg * min(wg_per_cu, -(-wgs // max(cus, 1))) / 4.0)
     rate = min(waves_per_simd / 4.0, 0.5)  # wave-instructions per cycle per SIMD
@@ -425,10 +430,10 @@ def main(argv=None):
                  else "spec_chunk+" + KERNEL_NAMES.get(plan["kernel"], "?") if args.level >= 2
                  else KERNEL_NAMES.get(plan["kernel"], "?"))
         pmc = None
-        if not args.no_pmc and world == 1 and args.level <= 1 and not args.paths and plan["kernel"] in (4, 5):
+        if not args.no_pmc and world == 1 and args.level <= 1 and not args.paths and plan["kernel"] in (4, 5, 6):
             largs = ["--model", args.model, "--ess", ess_name, "--replicate", str(args.replicate), "--steps", "3",
                      "--warmup", "1"]
-            kpref = "chain_viterbi_kernel" if plan["kernel"] == 4 else "pipe_viterbi_kernel"
+            kpref = {4: "chain_viterbi_kernel", 5: "pipe_viterbi_kernel", 6: "pipew_viterbi_kernel"}[plan["kernel"]]
             pmc = pmc_counters(largs, "void svh::(anonymous namespace)::" + kpref)
         rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc)
         workload = (f"{args.model} x {ess_name}" +
@@ -452,7 +457,8 @@ def main(argv=None):
                 "workload": workload, "states": n, "nnz": nnz, "sequences_per_gpu": len(seqs),
                 "observations_per_gpu": sum(lengths), "state_updates_per_gpu": updates_per_rank, "level": args.level,
                 "kernel": kname, "threads": plan["threads"], "slots": plan["slots"], "paths": bool(args.paths),
-                "workgroups_per_sequence": int(info["pipe_groups"]) if plan["kernel"] == 5 else 1,
+                "workgroups_per_sequence": (int(info["pipe_groups"]) if plan["kernel"] == 5 else
+                                            int(info["pipew_blocks"]) if plan["kernel"] == 6 else 1),
                 "fallback_rows": fallbacks,
                 "heavy_rows": plan["heavy_rows"], "spec_prep_s": None if prep_s is None else round(prep_s, 4),
                 "golden_checked": golden_checked,

@@ -191,6 +191,7 @@ struct PipeModel {
     int rowF, rowS;         // heavy rows (rowS < 0: the model has no sink row)
     float startF, startS;
     uint32_t n, S, P, nblk, SM, W, G;  // P = nblk*64*SM positions, G workgroups per sequence
+    uint32_t cus;           // wide plan: CUs of the device (W = waves per workgroup at most)
     uint32_t sx;            // S has a term from F
     uint32_t* fault;        // set non-zero if a bounded wait gave up
     unsigned long long* stamps;  // diagnostics (SVH_PIPE_DEBUG): [ticket][W][8] counters, or null
@@ -223,6 +224,19 @@ inline size_t pipew_lds_bytes(uint32_t SM, uint32_t W, uint32_t S, bool sx) {
     return (size_t)S * pipew_chunks(SM, sx) * 64 * 16 + (size_t)W * 8 * 64 * 4 + 16;
 }
 bool pipew_supported(int sm, int waves, bool sx);
+// Sequences (waves) per workgroup of a wide launch over nseq rows: the fewest of 1, 2, 4, 8, 12,
+// 16 that give about one workgroup per CU (a workgroup holds a CU's LDS), at most m.W.
+inline uint32_t pipew_waves_for(const PipeModel& m, uint64_t nseq) {
+    const uint64_t need = (nseq * m.nblk + m.cus - 1) / (m.cus ? m.cus : 1);
+    static const uint32_t ws[] = {1, 2, 4, 8, 12, 16};
+    uint32_t w = m.W;
+    for (uint32_t c : ws)
+        if (c >= need) {
+            w = c < m.W ? c : m.W;
+            break;
+        }
+    return w;
+}
 hipError_t launch_pipew(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
 
 // CSR of T^T used by the generic kernel and the _spec precompute.

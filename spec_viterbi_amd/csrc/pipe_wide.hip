@@ -87,7 +87,9 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
     const uint32_t id = (uint32_t)uniform((int)*tick);
     const uint32_t qg = id / nblk, blk = id - qg * nblk;
     {
+        // (unrolled: a one-wave workgroup would otherwise wait for each 1 KiB in turn)
         const f4* src = reinterpret_cast<const f4*>(m.tab) + (size_t)blk * S * NC * 64;
+#pragma unroll 8
         for (uint32_t i = tid; i < S * NC * 64; i += 64 * W) tabl[i] = src[i];
     }
     __syncthreads();
@@ -485,6 +487,9 @@ const void* pipew_fn(int sm, int waves, bool sx) {
         case 816: return pipew_ptr<8, 16>(sx);
         case 812: return pipew_ptr<8, 12>(sx);
         case 808: return pipew_ptr<8, 8>(sx);
+        case 804: return pipew_ptr<8, 4>(sx);
+        case 802: return pipew_ptr<8, 2>(sx);
+        case 801: return pipew_ptr<8, 1>(sx);
         default: return nullptr;
     }
 }
@@ -494,8 +499,9 @@ const void* pipew_fn(int sm, int waves, bool sx) {
 bool pipew_supported(int sm, int waves, bool sx) { return pipew_fn(sm, waves, sx) != nullptr; }
 
 hipError_t launch_pipew(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream) {
-    const void* fn = pipew_fn((int)m.SM, (int)m.W, m.sx != 0);
-    const size_t lds = pipew_lds_bytes(m.SM, m.W, m.S, m.sx != 0);
+    const uint32_t W = pipew_waves_for(m, b.nseq);
+    const void* fn = pipew_fn((int)m.SM, (int)W, m.sx != 0);
+    const size_t lds = pipew_lds_bytes(m.SM, W, m.S, m.sx != 0);
     if (!fn || m.S > 32 || m.nblk == 0 || m.G != m.nblk || m.P != m.nblk * 64 * m.SM || !x.ctr ||
         b.nseq > x.rows || x.G < m.nblk || lds > 160 * 1024)
         return hipErrorInvalidValue;
@@ -506,13 +512,14 @@ hipError_t launch_pipew(const PipeModel& m, const FusedBatch& b, const PipeScrat
         if (e != hipSuccess) return e;
     }
     PipeModel mm = m;
+    mm.W = W;
     FusedBatch bb = b;
     PipeScratch xx = x;
     const void* hc = m.hc;
     void* args[] = {&mm, &bb, &xx, &hc};
-    const uint64_t grid = ((uint64_t)b.nseq + m.W - 1) / m.W * m.nblk;
+    const uint64_t grid = ((uint64_t)b.nseq + W - 1) / W * m.nblk;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    return hipLaunchKernel(fn, dim3((uint32_t)grid), dim3(64 * m.W), args, lds, stream);
+    return hipLaunchKernel(fn, dim3((uint32_t)grid), dim3(64 * W), args, lds, stream);
 }
 
 }  // namespace svh

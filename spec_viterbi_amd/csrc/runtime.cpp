@@ -898,7 +898,12 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
         }
         if (bpl.ok && pipe.plan.ok && !(std::getenv("SVH_PIPEW") && std::atoi(std::getenv("SVH_PIPEW")) == 0)) {
             const PipePlan wpl = make_pipe_plan(host, 0, 0, true);
-            if (wpl.ok) pipe_wide.upload(wpl, host.n, host.S, stream);
+            if (wpl.ok) {
+                pipe_wide.upload(wpl, host.n, host.S, stream);
+                int cus = 0;
+                hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device), "CU count");
+                pipe_wide.view.cus = (uint32_t)cus;
+            }
         }
         if ((kernel_pref == SVH_KERNEL_PIPE && !pipe.plan.ok) || (kernel_pref == SVH_KERNEL_PIPE_WIDE && !pipe_wide.plan.ok))
             throw Error(SVH_E_UNSUPPORTED, "pipelined kernel requested but the model does not qualify (chain shape "
@@ -914,9 +919,11 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
         hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device), "CU count");
         cu_count = (uint32_t)cus;
         if (pipe.plan.ok) {
-            // AUTO: the pipelined plan while the batch holds at most two of its workgroups per CU
-            // (beyond that the chain kernel's higher throughput per CU wins); SVH_PIPE_MAX_NSEQ overrides
-            pipe_max_nseq = std::max<uint32_t>(1, 2 * cu_count / pipe.plan.G);
+            // AUTO: the latency plan while the batch gives every CU at most one of its workgroups
+            // (one wave per SIMD); wider batches run the wide pipelined plan (measured: DESIGN.md
+            // 5c), or the chain kernel where the model has none; SVH_PIPE_MAX_NSEQ overrides
+            pipe_max_nseq = std::max<uint32_t>(1, cu_count / pipe.plan.G);
+            if (!pipe_wide.plan.ok) pipe_max_nseq = std::max<uint32_t>(1, 2 * cu_count / pipe.plan.G);
             if (const char* e = std::getenv("SVH_PIPE_MAX_NSEQ")) pipe_max_nseq = (uint32_t)std::atoi(e);
         }
         if (pipe_wide.plan.ok) {
@@ -1087,10 +1094,11 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
     i.wide_slots = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.SM : 0;
     i.cu_count = cu_count;
     if (ppl) {
+        const uint32_t w = ppl->plan.wide ? pipew_waves_for(ppl->view, nseq) : ppl->plan.W;
         i.kernel = ppl->plan.wide ? SVH_KERNEL_PIPE_WIDE : SVH_KERNEL_PIPE;
-        i.threads = (int32_t)(64 * ppl->plan.W);
+        i.threads = (int32_t)(64 * w);
         i.slots = (int32_t)ppl->plan.SM;
-        i.lds_bytes = ppl->plan.wide ? pipew_lds_bytes(ppl->plan.SM, ppl->plan.W, host.S, ppl->plan.sx)
+        i.lds_bytes = ppl->plan.wide ? pipew_lds_bytes(ppl->plan.SM, w, host.S, ppl->plan.sx)
                                      : pipe_lds_bytes(ppl->plan.W, host.S);
     }
     if (pipe_wide.plan.ok) {

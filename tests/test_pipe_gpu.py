@@ -38,6 +38,12 @@ def run(hmm, seqs, kernel=_lib.SVH_KERNEL_PIPE, level=0):
     return s, best, (b.fallbacks() if kernel in PIPES else 0), plan
 
 
+def pipew_waves(info, nseq):
+    """Sequences per workgroup of a wide launch (kernels.h pipew_waves_for)."""
+    need = -(-nseq * info["pipew_blocks"] // info["cu_count"])
+    return next((min(c, info["pipew_waves"]) for c in (1, 2, 4, 8, 12, 16) if c >= need), info["pipew_waves"])
+
+
 def assert_same(s1, b1, s2, b2):
     for q in range(len(s1)):
         assert bit_equal(s1[q], s2[q]), (q, first_mismatch(s1[q], s2[q]))
@@ -82,7 +88,9 @@ def test_pipe_auto_selects_pipe_for_small_batches():
     wide = model.batch(random_seqs(20, [8] * (info["pipe_max_nseq"] + 1), seed=2))
     assert info["pipew_min_nseq"] == info["pipe_max_nseq"] + 1 and info["pipew_blocks"] == 5, info
     assert wide.plan()["kernel"] == _lib.SVH_KERNEL_PIPE_WIDE
-    assert wide.plan()["threads"] == 64 * info["pipew_waves"] and wide.plan()["slots"] == info["pipew_slots"]
+    w = pipew_waves(info, info["pipe_max_nseq"] + 1)
+    assert wide.plan()["threads"] == 64 * w and wide.plan()["slots"] == info["pipew_slots"]
+    assert pipew_waves(info, 8000) == 16 and pipew_waves(info, 50) == 1
     # the chain kernel forced: its wide plan
     chain = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_CHAIN).batch(random_seqs(20, [8] * 300, seed=3))
     assert chain.plan()["kernel"] == _lib.SVH_KERNEL_CHAIN
@@ -169,15 +177,22 @@ def test_pipe_chain_variants(variant, kern):
     oracle_check(hmm, seqs, s, b)
 
 
-@pytest.mark.parametrize("waves", [8, 12, 16])
-def test_pipew_geometries(waves, monkeypatch):
-    """Wide plan with 8, 12 and 16 sequences per workgroup: ragged batch wider than one workgroup."""
-    monkeypatch.setenv("SVH_PIPEW_WAVES", str(waves))
+@pytest.mark.parametrize("waves", [1, 2, 4, 8, 12, 16])
+def test_pipew_geometries(waves):
+    """Wide plan with 1 .. 16 sequences per workgroup, the count the batch width selects (about
+    one workgroup per CU): ragged batches, equal to the chain kernel, a sample against the oracle."""
     hmm = random_chain_hmm(1300, S=20, seed=23, n_from_m=False)
-    seqs = random_seqs(20, [500, 129, 2, 64, 1030] * 5, seed=24)
+    info = svh.DeviceModel(hmm).info()
+    nseq = waves * info["cu_count"] // info["pipew_blocks"]
+    rng = np.random.default_rng(waves)
+    lens = [500, 129, 2, 64, 1030] + list(rng.integers(1, 90, size=nseq - 5))
+    seqs = random_seqs(20, lens, seed=24)
     s, b, fb, plan = run(hmm, seqs, kernel=_lib.SVH_KERNEL_PIPE_WIDE)
-    assert plan["pipew_waves"] == waves and plan["threads"] == 64 * waves and fb == 0
-    oracle_check(hmm, seqs, s, b)
+    assert pipew_waves(info, nseq) == waves and plan["threads"] == 64 * waves and fb == 0, plan
+    sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
+    assert_same(s, b, sc, bc)
+    sample = [0, 1, 2, 3, 4, nseq - 1]
+    oracle_check(hmm, [seqs[q] for q in sample], s[sample], b[sample])
 
 
 @pytest.mark.parametrize("geom", [(1, 4), (1, 8), (2, 4), (2, 8)])
