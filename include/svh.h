@@ -206,6 +206,9 @@ int svh_decode_file(svh_model_t m, const char* path, int format, uint32_t level,
                     uint64_t* nseq_total);
 
 /* ---- one-shot convenience: upload, run, download --------------------------------------- */
+/* The model keeps the batch it used (one for scores only, one with paths) and reloads it on the
+ * next call: device buffers only grow, so repeated calls allocate and free nothing.  Calls on one
+ * model are serialised. */
 int svh_viterbi(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* offsets,
                 const uint64_t* symbols, float* scores, int64_t* best_state, int32_t* paths);
 

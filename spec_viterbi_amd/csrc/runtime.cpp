@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <map>
 #include <memory>
@@ -614,9 +615,6 @@ void DeviceBandPlan::upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream
     view.SM = p.SM;
     view.erow = p.erow;
     view.H = p.H;
-    d_fault.alloc(4);
-    hip_check(hipMemsetAsync(d_fault.ptr, 0, 4, s), "fault word");
-    view.fault = d_fault.as<uint32_t>();
     const char* dbg = std::getenv("SVH_BAND_DEBUG");  // diagnostic ablations only
     view.dbg = dbg ? (uint32_t)std::atoi(dbg) : 0u;
     if (view.dbg & (4u | 128u)) {
@@ -739,8 +737,6 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     d_start.upload(p.start.data(), p.start.size() * 4, s);
     d_lrow.upload(p.lrow.data(), p.lrow.size() * 4, s);
     d_hc.upload(p.hc.data(), p.hc.size() * 4, s);
-    d_fault.alloc(4);
-    hip_check(hipMemsetAsync(d_fault.ptr, 0, 4, s), "fault word");
     std::memset(&view, 0, sizeof(view));
     view.tab = d_tab.as<float2>();
     view.e0 = d_e0.as<float>();
@@ -759,7 +755,6 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     view.W = p.W;
     view.G = p.G;
     view.sx = p.sx ? 1u : 0u;
-    view.fault = d_fault.as<uint32_t>();
     if (const char* e = std::getenv("SVH_PIPE_DEBUG"); e && std::atoi(e)) {  // diagnostics only
         d_stamps.alloc((size_t)65536 * kPipeStamps * 8);
         hip_check(hipMemsetAsync(d_stamps.ptr, 0, d_stamps.bytes, s), "stamps");
@@ -915,6 +910,12 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
             BandPlan wide = make_band_plan(host, 0, true, 4);
             if (wide.ok) band_wide.upload(wide, host.n, host.S, stream);
         }
+        d_faults.alloc(4 * sizeof(uint32_t));
+        hip_check(hipMemsetAsync(d_faults.ptr, 0, d_faults.bytes, stream), "fault words");
+        pipe.view.fault = d_faults.as<uint32_t>() + 0;
+        pipe_wide.view.fault = d_faults.as<uint32_t>() + 1;
+        band.view.fault = d_faults.as<uint32_t>() + 2;
+        band_wide.view.fault = d_faults.as<uint32_t>() + 3;
         int cus = 0;
         hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device), "CU count");
         cu_count = (uint32_t)cus;
@@ -1387,46 +1388,64 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
     d_S.reserve((size_t)nseq * n * 4);
     d_Y.reserve((size_t)nv * n * 4);
     d_vbest.reserve((size_t)2 * nv * nb * 8);
-    // One launch of the step kernel over rows (begin, end, v_in row) of the batch's sequences.
-    // Nothing here waits for the device: every launch's row tables get device buffers of their
-    // own (sized up front, so none is reallocated under a pending kernel) and their host copies
-    // live until the end of the run; begin/end may instead come from the device (fallbacks).
-    std::vector<std::unique_ptr<DeviceBuffer>> dev_keep;
-    std::vector<std::vector<uint64_t>> host_keep64;
-    std::vector<std::vector<uint32_t>> host_keep32;
+    uint32_t nflags = 0;
+    DeviceBuffer d_fbeg, d_fend, d_arena;
+    d_fbeg.reserve((size_t)nv * 4);
+    d_fend.reserve((size_t)nv * 4);
+    d_flag.reserve((size_t)nv * 4);
+    // Every row table of the run (sequence offsets, begin / end / v_in rows, correction rows) is
+    // packed into one host arena first and the device work recorded as operations on the arena's
+    // device copy; then one upload and the operations back to back, so the timed region carries
+    // no per-table allocation or copy (the launch sequence itself waits for nothing: the
+    // fallbacks' begin / end come from the device).
+    std::vector<uint8_t> arena;
+    std::vector<std::function<void(const uint8_t*)>> ops;  // argument: the arena's device base
+    constexpr size_t kNone = ~(size_t)0;
+    auto put = [&](const void* p, size_t bytes) -> size_t {
+        const size_t off = (arena.size() + 15) & ~(size_t)15;
+        arena.resize(off + std::max<size_t>(bytes, 1));
+        if (bytes) std::memcpy(arena.data() + off, p, bytes);
+        return off;
+    };
+    auto table32 = [&](std::vector<uint32_t>& v) -> size_t {
+        const size_t off = put(v.data(), v.size() * 4);
+        v.clear();
+        return off;
+    };
+    auto at32 = [](const uint8_t* base, size_t off) { return reinterpret_cast<const uint32_t*>(base + off); };
     std::vector<uint64_t> vsym;
     std::vector<uint32_t> vbeg, vend, vrow;
-    auto table32 = [&](std::vector<uint32_t>& v) -> const uint32_t* {
-        host_keep32.push_back(std::move(v));
-        v.clear();
-        dev_keep.push_back(std::make_unique<DeviceBuffer>());
-        dev_keep.back()->upload_async(host_keep32.back().data(), host_keep32.back().size() * 4, s);
-        return dev_keep.back()->as<uint32_t>();
-    };
+    // One launch of the step kernel over rows (begin, end, v_in row) of the batch's sequences;
+    // begin/end may instead come from the device (fallbacks).
     auto launch_rows = [&](const float* v_in, float* out, const uint32_t* dbeg = nullptr,
                            const uint32_t* dend = nullptr) {
         const uint32_t rows = (uint32_t)vsym.size();
         if (rows == 0) return;
-        host_keep64.push_back(std::move(vsym));
+        const size_t osym = put(vsym.data(), (size_t)rows * 8);
         vsym.clear();
-        dev_keep.push_back(std::make_unique<DeviceBuffer>());
-        dev_keep.back()->upload_async(host_keep64.back().data(), (size_t)rows * 8, s);
-        FusedBatch fb;
-        std::memset(&fb, 0, sizeof(fb));
-        fb.symbols = d_sym.as<uint8_t>();
-        fb.sym_off = dev_keep.back()->as<uint64_t>();
-        fb.begin = dbeg ? dbeg : table32(vbeg);
-        fb.end = dend ? dend : table32(vend);
-        fb.v_in = v_in;
-        fb.v_in_row = table32(vrow);
-        fb.scores = out;
-        fb.best = d_vbest.as<int64_t>();
-        fb.nseq = rows;
+        const size_t ob = dbeg ? kNone : table32(vbeg);
+        const size_t oe = dend ? kNone : table32(vend);
+        const size_t orow = table32(vrow);
         vbeg.clear();
         vend.clear();
-        model->launch_steps(fb, false, s);
+        const uint8_t* sym = d_sym.as<uint8_t>();
+        int64_t* vbest = d_vbest.as<int64_t>();
+        Model* mdl = model;
+        ops.push_back([=](const uint8_t* base) {
+            FusedBatch fb;
+            std::memset(&fb, 0, sizeof(fb));
+            fb.symbols = sym;
+            fb.sym_off = reinterpret_cast<const uint64_t*>(base + osym);
+            fb.begin = dbeg ? dbeg : at32(base, ob);
+            fb.end = dend ? dend : at32(base, oe);
+            fb.v_in = v_in;
+            fb.v_in_row = at32(base, orow);
+            fb.scores = out;
+            fb.best = vbest;
+            fb.nseq = rows;
+            mdl->launch_steps(fb, false, s);
+        });
     };
-    hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
     // 1a: probes from the guesses, rows v * nb + b (segment 0: from the start column, and its
     // basis rows are unused zero-step copies)
     for (const Seg& x : segs) {
@@ -1451,6 +1470,12 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
         }
     }
     launch_rows(d_G.as<float>(), d_E1.as<float>());
+    float* const S_ = d_S.as<float>();
+    float* const P_ = d_P.as<float>();
+    float* const X_ = d_X.as<float>();
+    float* const Y_ = d_Y.as<float>();
+    const float* const G_ = d_G.as<float>();
+    const float* const E1_ = d_E1.as<float>();
     // S[q] = end of segment 0 (exact)
     {
         std::vector<uint32_t> irow(nseq), orow(nseq);
@@ -1458,19 +1483,18 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
             irow[q] = first_seg[q] * nb;
             orow[q] = q;
         }
-        const uint32_t* di = table32(irow);
-        const uint32_t* dout = table32(orow);
-        hip_check(launch_tp_copy_rows(d_E1.as<float>(), di, d_S.as<float>(), dout, nseq, n, nullptr, s),
-                  "time-parallel copy");
+        const size_t di = table32(irow), dout = table32(orow);
+        const uint32_t ns = nseq;
+        ops.push_back([=](const uint8_t* base) {
+            hip_check(launch_tp_copy_rows(E1_, at32(base, di), S_, at32(base, dout), ns, n, nullptr, s),
+                      "time-parallel copy");
+        });
     }
     // 2: segments 1, 2, ... in order, all sequences at once.  The correction kernel decides on
     // the device which segments are re-run: it writes each fallback row's (begin, end), a
     // converged segment's row has no steps, and only flagged rows are copied into S.
-    uint32_t nflags = 0;
-    DeviceBuffer d_fbeg, d_fend;
-    d_fbeg.reserve((size_t)nv * 4);
-    d_fend.reserve((size_t)nv * 4);
-    d_flag.reserve((size_t)nv * 4);
+    uint32_t* const fbeg_ = d_fbeg.as<uint32_t>();
+    uint32_t* const fend_ = d_fend.as<uint32_t>();
     for (uint32_t k = 1; k < kmax; ++k) {
         std::vector<uint32_t> act;  // virtual segment ids of segment k
         for (uint32_t q = 0; q < nseq; ++q)
@@ -1479,7 +1503,12 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
         const uint32_t na = (uint32_t)act.size();
         // probes from the exact start S[q] -> X rows 0..na-1, and (with basis rows) from its light
         // part -> X rows na..2na-1
-        hip_check(launch_tp_probe_starts(d_S.as<float>(), d_P.as<float>(), nseq, n, basis, s), "time-parallel starts");
+        {
+            const uint32_t ns = nseq;
+            ops.push_back([=](const uint8_t*) {
+                hip_check(launch_tp_probe_starts(S_, P_, ns, n, basis, s), "time-parallel starts");
+            });
+        }
         std::vector<uint32_t> rx(na), rg(na), re(na), ro(na), rf(na), rp(na), rs(na);
         for (uint32_t part = 0; part < (basis.H ? 2u : 1u); ++part) {
             for (uint32_t a = 0; a < na; ++a) {
@@ -1497,29 +1526,46 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
                 rs[a] = x.e;
             }
         }
-        launch_rows(d_P.as<float>(), d_X.as<float>());
+        launch_rows(P_, X_);
         std::vector<uint32_t> ya(na);
         for (uint32_t a = 0; a < na; ++a) ya[a] = a;
-        TpRows tr{table32(rx), table32(rg), table32(re), table32(ro), table32(rf), table32(rp), table32(rs)};
-        uint32_t* flag = d_flag.as<uint32_t>() + nflags;
-        hip_check(launch_tp_correct(d_X.as<float>(), d_G.as<float>(), d_E1.as<float>(), tr, na, basis.H ? na : 0,
-                                    basis, d_S.as<float>(), n, tol, flag, d_fbeg.as<uint32_t>(),
-                                    d_fend.as<uint32_t>(), s),
-                  "time-parallel correction");
+        const size_t o_rx = table32(rx), o_rg = table32(rg), o_re = table32(re), o_ro = table32(ro),
+                     o_rf = table32(rf), o_rp = table32(rp), o_rs = table32(rs);
+        uint32_t* const flag = d_flag.as<uint32_t>() + nflags;
+        ops.push_back([=](const uint8_t* base) {
+            const TpRows tr{at32(base, o_rx), at32(base, o_rg), at32(base, o_re), at32(base, o_ro),
+                            at32(base, o_rf), at32(base, o_rp), at32(base, o_rs)};
+            hip_check(launch_tp_correct(X_, G_, E1_, tr, na, basis.H ? na : 0, basis, S_, n, tol, flag, fbeg_,
+                                        fend_, s),
+                      "time-parallel correction");
+        });
         // fallbacks: the rest of each flagged segment from X, exactly, into Y, then into S
         for (uint32_t a = 0; a < na; ++a) {
             const Seg& x = segs[act[a]];
             vsym.push_back(h_symoff[x.q]);
             vrow.push_back(a);
         }
-        launch_rows(d_X.as<float>(), d_Y.as<float>(), d_fbeg.as<uint32_t>(), d_fend.as<uint32_t>());
-        const uint32_t* dya = table32(ya);
-        hip_check(launch_tp_copy_rows(d_Y.as<float>(), dya, d_S.as<float>(), tr.out, na, n, flag, s),
-                  "time-parallel copy");
+        launch_rows(X_, Y_, fbeg_, fend_);
+        const size_t o_ya = table32(ya);
+        ops.push_back([=](const uint8_t* base) {
+            hip_check(launch_tp_copy_rows(Y_, at32(base, o_ya), S_, at32(base, o_ro), na, n, flag, s),
+                      "time-parallel copy");
+        });
         nflags += na;
     }
-    hip_check(launch_tp_finish(d_S.as<float>(), d_scores.as<float>(), d_best.as<int64_t>(), nseq, n, s),
-              "time-parallel finish");
+    {
+        int64_t* const best_ = d_best.as<int64_t>();
+        float* const scores_ = d_scores.as<float>();
+        const uint32_t ns = nseq;
+        ops.push_back([=](const uint8_t*) {
+            hip_check(launch_tp_finish(S_, scores_, best_, ns, n, s), "time-parallel finish");
+        });
+    }
+    d_arena.reserve(arena.size());
+    hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
+    hip_check(hipMemcpyAsync(d_arena.ptr, arena.data(), arena.size(), hipMemcpyHostToDevice, s), "time-parallel rows");
+    const uint8_t* const base = d_arena.as<uint8_t>();
+    for (auto& op : ops) op(base);
     hip_check(hipEventRecord(ev_stop, s), "hipEventRecord");
     std::vector<uint32_t> flags(nflags);
     if (nflags)
@@ -1537,12 +1583,22 @@ void Batch::read(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out
     if (!s) s = model->stream;
     if (!ran) throw Error(SVH_E_STATE, "svh_batch_read before svh_batch_run");
     if (paths_out && !paths) throw Error(SVH_E_STATE, "batch was created without SVH_BATCH_PATHS");
+    // scores, best states and the model's fault words into pinned staging on the run's stream,
+    // one synchronisation, then out to the caller (pageable copies would each block on their own)
+    const size_t sb = scores ? (size_t)nseq * model->host.n * 4 : 0, bb = best ? (size_t)nseq * 8 : 0;
+    const size_t fb = model->d_faults.ptr ? 4 * sizeof(uint32_t) : 0;
+    uint8_t* st = h_out.reserve(fb + sb + bb);
+    if (fb) hip_check(hipMemcpyAsync(st, model->d_faults.ptr, fb, hipMemcpyDeviceToHost, s), "fault D2H");
+    if (sb) hip_check(hipMemcpyAsync(st + fb, d_scores.ptr, sb, hipMemcpyDeviceToHost, s), "scores D2H");
+    if (bb) hip_check(hipMemcpyAsync(st + fb + sb, d_best.ptr, bb, hipMemcpyDeviceToHost, s), "best D2H");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-    model->check_fault();
-    if (scores)
-        hip_check(hipMemcpy(scores, d_scores.ptr, (size_t)nseq * model->host.n * 4, hipMemcpyDeviceToHost),
-                  "scores D2H");
-    if (best) hip_check(hipMemcpy(best, d_best.ptr, (size_t)nseq * 8, hipMemcpyDeviceToHost), "best D2H");
+    if (fb) {
+        uint32_t f[4];
+        std::memcpy(f, st, sizeof(f));
+        model->report_faults(f);
+    }
+    if (sb) std::memcpy(scores, st + fb, sb);
+    if (bb) std::memcpy(best, st + fb + sb, bb);
     if (paths_out)
         hip_check(hipMemcpy(paths_out, d_paths.ptr, (size_t)total * 4, hipMemcpyDeviceToHost), "paths D2H");
 }
@@ -1597,24 +1653,18 @@ void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) co
 }
 
 void Model::check_fault() const {
-    for (const DevicePipePlan* p : {&pipe, &pipe_wide}) {
-        if (!p->plan.ok || !p->view.fault) continue;
-        uint32_t fault = 0;
-        hip_check(hipMemcpy(&fault, p->view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
-        if (fault) {
-            hip_check(hipMemset(p->view.fault, 0, 4), "fault reset");
-            throw Error(SVH_E_HIP, "pipelined kernel: a bounded wait gave up (results invalid)");
-        }
-    }
-    for (const DeviceBandPlan* p : {&band, &band_wide}) {
-        if (!p->plan.ok || !p->view.fault) continue;
-        uint32_t fault = 0;
-        hip_check(hipMemcpy(&fault, p->view.fault, 4, hipMemcpyDeviceToHost), "fault D2H");
-        if (fault) {
-            // reported once: clear the word so the model's later runs are judged on their own
-            hip_check(hipMemset(p->view.fault, 0, 4), "fault reset");
-            throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
-        }
+    if (!d_faults.ptr) return;  // no chain / pipelined plan
+    uint32_t f[4] = {0, 0, 0, 0};
+    hip_check(hipMemcpy(f, d_faults.ptr, sizeof(f), hipMemcpyDeviceToHost), "fault D2H");
+    report_faults(f);
+}
+
+void Model::report_faults(const uint32_t* f) const {
+    if (f[0] | f[1] | f[2] | f[3]) {
+        // reported once: clear the words so the model's later runs are judged on their own
+        hip_check(hipMemset(d_faults.ptr, 0, 4 * sizeof(uint32_t)), "fault reset");
+        if (f[0] | f[1]) throw Error(SVH_E_HIP, "pipelined kernel: a bounded wait gave up (results invalid)");
+        throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
     }
 }
 

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <mutex>
 #include <stdexcept>
@@ -118,7 +119,7 @@ BandPlan make_band_plan(const HostModel& hm, int max_threads, bool chain, int ge
 
 struct DeviceBandPlan {
     BandPlan plan;
-    DeviceBuffer d_erows, d_erows_t, d_start, d_aw, d_bw, d_lrow, d_stamps, d_fault, d_pflags, d_spos;
+    DeviceBuffer d_erows, d_erows_t, d_start, d_aw, d_bw, d_lrow, d_stamps, d_pflags, d_spos;
     BandModel view{};
     void upload(const BandPlan& p, uint32_t n, uint32_t S, hipStream_t s);
     void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_BAND_DEBUG & 4)
@@ -144,10 +145,34 @@ PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm = 0, uint32_t waves = 0
 
 struct DevicePipePlan {
     PipePlan plan;
-    DeviceBuffer d_tab, d_e0, d_start, d_lrow, d_hc, d_fault, d_stamps;
+    DeviceBuffer d_tab, d_e0, d_start, d_lrow, d_hc, d_stamps;
     PipeModel view{};
     void upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream_t s);
     void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_PIPE_DEBUG): first sequence's waves
+};
+
+// Pinned host staging buffer (grow-only).
+template <class T>
+struct Pinned {
+    T* p = nullptr;
+    size_t n = 0;
+    Pinned() = default;
+    Pinned(const Pinned&) = delete;
+    Pinned& operator=(const Pinned&) = delete;
+    ~Pinned() {
+        if (p) (void)hipHostFree(p);
+    }
+    T* reserve(size_t count) {
+        if (count > n) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            n = 0;
+            hip_check(hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault),
+                      "hipHostMalloc");
+            n = count;
+        }
+        return p;
+    }
 };
 
 // Scratch of the pipelined kernel, owned by a batch (grow-only).
@@ -179,6 +204,9 @@ struct Model {
     uint32_t spec_level = 0;
     uint32_t pstride = 0;
     DeviceBuffer d_mfold, d_products;
+    // fault words of the bounded waits, one per chain / pipelined plan (pipe, pipe_wide, band,
+    // band_wide): one allocation, so check_fault reads them with a single copy
+    DeviceBuffer d_faults;
 
     Model(const HostModel& h, const svh_model_opts* opts);
     ~Model();
@@ -191,8 +219,11 @@ struct Model {
     const DevicePipePlan* pipe_for(uint32_t nseq) const;
     void spec_build(uint32_t level, hipStream_t s);
     svh_model_info info(uint32_t nseq = 0, bool paths = false, uint32_t level = 0) const;
-    // throws if a chain-kernel bounded wait gave up since the model was created (synchronous)
+    // throws if a bounded wait of a chain / pipelined kernel gave up since the last check
+    // (synchronous; the words are cleared when reported)
     void check_fault() const;
+    // the same for fault words already copied to the host (f: d_faults' 4 words)
+    void report_faults(const uint32_t* f) const;
     // one pass of the step kernel the model plans for (chain, band, fused or generic)
     void launch_steps(const FusedBatch& b, bool paths, hipStream_t s) const;
 };
@@ -218,6 +249,7 @@ struct Batch {
 
     // host staging of the last load (kept alive for the asynchronous uploads)
     std::vector<uint8_t> h_sym;
+    Pinned<uint8_t> h_out;  // read(): scores, best and the fault words land here in one sync
     std::vector<uint64_t> h_symoff, h_pathoff, h_bpoff, h_cmoff, h_hroff, h_ckoff;
     std::vector<uint32_t> h_zero;
 

@@ -74,25 +74,6 @@ class ChunkQueue {
     std::exception_ptr err_;
 };
 
-template <class T>
-struct Pinned {
-    T* p = nullptr;
-    size_t n = 0;
-    ~Pinned() {
-        if (p) (void)hipHostFree(p);
-    }
-    T* reserve(size_t count) {
-        if (count > n) {
-            if (p) (void)hipHostFree(p);
-            p = nullptr;
-            hip_check(hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault),
-                      "hipHostMalloc");
-            n = count;
-        }
-        return p;
-    }
-};
-
 struct Slot {
     std::unique_ptr<Batch> batch;
     Chunk chunk;

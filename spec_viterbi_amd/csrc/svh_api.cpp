@@ -2,6 +2,7 @@
 // thread-local message and returns a status code: no exception crosses the ABI.
 #include <fstream>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 
@@ -19,6 +20,11 @@ struct svh_ess {
 };
 struct svh_model {
     std::unique_ptr<svh::Model> impl;
+    // svh_viterbi's batches (scores only / with paths), kept between calls: their device buffers
+    // only grow, so a one-shot call after the first allocates nothing and frees nothing (no
+    // hipMalloc / hipFree device-wide syncs on the drop-in run_Viterbi path)
+    std::mutex oneshot_mu;
+    std::unique_ptr<svh::Batch> oneshot[2];
 };
 struct svh_batch {
     std::unique_ptr<svh::Batch> impl;
@@ -278,9 +284,12 @@ int svh_viterbi(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* of
                 const uint64_t* symbols, float* scores, int64_t* best_state, int32_t* paths) {
     return guarded([&] {
         require(m != nullptr, "null model");
-        svh::Batch b(m->impl.get(), nseq, offsets, symbols, paths ? SVH_BATCH_PATHS : 0u);
-        b.run(level, nullptr);
-        b.read(nullptr, scores, best_state, paths);
+        std::lock_guard<std::mutex> lock(m->oneshot_mu);
+        std::unique_ptr<svh::Batch>& b = m->oneshot[paths ? 1 : 0];
+        if (b) b->load(nseq, offsets, symbols, nullptr, m->impl->stream);
+        else b = std::make_unique<svh::Batch>(m->impl.get(), nseq, offsets, symbols, paths ? SVH_BATCH_PATHS : 0u);
+        b->run(level, nullptr);
+        b->read(nullptr, scores, best_state, paths);
     });
 }
 

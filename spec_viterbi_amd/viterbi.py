@@ -110,7 +110,9 @@ class DeviceBatch:
         to 1.4e-5 relative on 2405 x covid-19, DESIGN.md 6b -- not bit-exact, unlike run()).
         `rel_tol` is the convergence check's tolerance (when a segment's probe counts as
         converged), not a bound on the output error; rel_tol < 0 re-runs every segment and is
-        bit-exact.  Returns the number of segments re-run exactly."""
+        bit-exact.  Returns the number of segments re-run exactly.  On MSV-shaped models that the
+        pipelined plan runs, the serial run() is faster (2405 x covid-19: 0.66 vs 0.90 ms); the
+        pass pays on models the pipelined plans do not take."""
         fb = ctypes.c_uint64()
         _lib.check(_lib.lib.svh_batch_run_time_parallel(self._h, int(seg_len), int(probe_len), float(rel_tol),
                                                          ctypes.c_void_p(stream or 0), ctypes.byref(fb)))

@@ -413,3 +413,30 @@ def test_wide_plan_other_pfam_models(name):
         ref = oracle.viterbi(hmm, seqs[q])
         assert bit_equal(wide[q], ref), (q, first_mismatch(wide[q], ref))
         assert wide_best[q] == int(np.argmin(ref)), q
+
+
+def test_oneshot_batches_reused_across_calls():
+    """svh_viterbi keeps its batches between calls (grow-only device buffers): shrinking and
+    growing batches, a paths call, a rejected call and a level-1 call in between must each give
+    the oracle's results."""
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
+    model = svh.DeviceModel(hmm)
+    ref, _ = oracle.viterbi_batch(hmm, seqs, nthreads=16)
+    short = [s[:700] for s in seqs[:3]]
+    ref_short = [oracle.viterbi(hmm, s) for s in short]
+    for batch, expect in ((seqs, ref), (short, ref_short), (seqs[:1], ref[:1]), (seqs, ref)):
+        scores, best = model.viterbi(batch)
+        for q in range(len(batch)):
+            assert bit_equal(scores[q], expect[q]), (len(batch), q, first_mismatch(scores[q], expect[q]))
+            assert best[q] == int(np.argmin(expect[q]))
+    bad = [np.array([0, 1, 250], dtype=np.uint64)]
+    with pytest.raises(_lib.SvhError):
+        model.viterbi(bad)
+    scores, best, pth = model.viterbi(short, paths=True)
+    for q, s in enumerate(short):
+        r, rb, rp = oracle.decode(hmm, s)
+        assert bit_equal(scores[q], r) and best[q] == rb and np.array_equal(pth[q], rp), q
+    scores, _ = model.viterbi(seqs[:7], level=1)
+    for q in range(7):
+        assert bit_equal(scores[q], ref[q]), q
