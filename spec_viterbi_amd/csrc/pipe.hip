@@ -332,6 +332,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 bprev = readlane_f(ring_prev[((first - 1) & (kR - 1)) * 64 + 63], 0);
             } else if constexpr (SRC == 2) {
                 bprev = gran_value(first - 1);
+                // initial progress (observations < first are done): a row that starts mid-sequence
+                // at a multiple of 64 would otherwise leave its producer's first flow-control wait
+                // on a stale word while this wave waits for that producer's granules
+                if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | first);
             }
 
             uint32_t t = first;

@@ -279,7 +279,13 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
                 ring_w[((first - 1) & 7u) * 64 + lane] = vp[NP - 1].y;
                 put_gran1(first - 1, readlane_f(vp[NP - 1].y, 63));
             }
-            if constexpr (SRC == 2) bprev = gran_value(first - 1);
+            if constexpr (SRC == 2) {
+                bprev = gran_value(first - 1);
+                // initial progress (observations < first are done): a row that starts mid-sequence
+                // at a multiple of 64 would otherwise leave its producer's first flow-control wait
+                // on a stale word while this wave waits for that producer's granules
+                if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | first);
+            }
 
             uint32_t t = first;
             for (; t < len && (t & 31u); ++t) single(t);
