@@ -268,3 +268,26 @@ def test_pipew_other_pfam_models_replicated(name):
     s, b, fb, plan = run(hmm, seqs, kernel=_lib.SVH_KERNEL_PIPE_WIDE)
     sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
     assert_same(s, b, sc, bc)
+
+
+def test_pipe_spec3_tail_starting_at_256():
+    """Regression for the pipelined kernels' initial progress word: a `_spec`
+    level-3 tail that starts at observation 256 (a multiple of 64 past the flow-control window)
+    and runs two observations, on a latency plan with two workgroups per sequence.  Before the
+    fix the producer's first flow-control wait and the consumer's first granule wait deadlocked
+    (a bounded-wait give-up).  Checked bit-exact against the serial chain kernel at level 3 and
+    within the reference's tolerance of the non-spec oracle."""
+    hmm = svh.read_HMM(chmm("1001.chmm"))
+    seq = svh.read_emit_seq(ess("emit_3_3500_20.ess"))[0][:258]
+    model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_PIPE)
+    info = model.info()
+    assert info["pipe_groups"] >= 2, info
+    model.spec_build(3)
+    got, _ = model.viterbi([seq], level=3)
+    model.close()
+    chain = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_CHAIN)
+    chain.spec_build(3)
+    ref, _ = chain.viterbi([seq], level=3)
+    chain.close()
+    assert bit_equal(got[0], ref[0]), first_mismatch(got[0], ref[0])
+    assert all(svh.almost_equal(a, b) for a, b in zip(got[0], oracle.viterbi(hmm, seq)))
