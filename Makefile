@@ -25,12 +25,13 @@ HDRS := $(wildcard $(CSRC)/*.h) $(wildcard include/*.h)
 CPP_TESTS := tests/cpp/test_HIP_impl tests/cpp/test_HIP_spec_impl tests/cpp/test_semantic_equality \
              tests/cpp/test_readers_asan
 
-.PHONY: all lib oracle ref tests clean
-all: lib oracle tests ref
+.PHONY: all lib oracle ref tests tools clean
+all: lib oracle tests tools ref
 
 lib: $(LIB)
 oracle: $(ORACLE)
 tests: $(CPP_TESTS)
+tools: tools/bench_harness
 
 $(BUILD):
 	mkdir -p $(BUILD)
@@ -55,6 +56,10 @@ tests/cpp/test_readers_asan: tests/cpp/test_readers_asan.cpp $(CSRC)/data_reader
 	$(CXX) -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -Iinclude -I$(CSRC) \
 		-o $@ tests/cpp/test_readers_asan.cpp $(CSRC)/data_reader.cpp $(CSRC)/seqreader.cpp
 
+# The reference benchmark harness's per-sequence call loop over HIP_impl / HIP_spec_impl.
+tools/bench_harness: tools/bench_harness.cpp $(LIB) include/HIP_impl.h include/HIP_spec_impl.h
+	$(HIPCC) $(HOSTFLAGS) -o $@ $< -L$(dir $(LIB)) -lspec_viterbi_hip -Wl,-rpath,'$$ORIGIN/../spec_viterbi_amd'
+
 # C++ tests written against the reference's interfaces (tests/cpp/*.cpp).
 tests/cpp/%: tests/cpp/%.cpp tests/cpp/test_helper.h $(LIB)
 	$(HIPCC) $(HOSTFLAGS) -o $@ $< -L$(dir $(LIB)) -lspec_viterbi_hip -Wl,-rpath,'$$ORIGIN/../../spec_viterbi_amd'
@@ -65,4 +70,4 @@ ref:
 	else echo "reference checkout not present: skipping oracle/_ref"; fi
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(ORACLE) $(CPP_TESTS) oracle/_ref
+	rm -rf $(BUILD) $(LIB) $(ORACLE) $(CPP_TESTS) tools/bench_harness oracle/_ref

@@ -173,6 +173,10 @@ int svh_batch_plan(svh_batch_t b, uint32_t level, svh_model_info* info);
  * did not use the pipelined kernel.  Waits for the run. */
 int svh_batch_fallbacks(svh_batch_t b, uint64_t* rows);
 int svh_batch_destroy(svh_batch_t b);
+/* Diagnostics: mark the batch's last run (enqueued on `stream`) as if one of its bounded waits
+ * had given up, so its next svh_batch_read fails with SVH_E_HIP.  Every batch has a fault word of
+ * its own that only its runs set and only its reads report and clear (tests of that isolation). */
+int svh_batch_debug_fault(svh_batch_t b, void* stream);
 
 /* Batch from uint8 symbols (the device format; e.g. straight from svh_reader_next). */
 int svh_batch_create_u8(svh_model_t m, uint64_t nseq, const uint64_t* offsets,

@@ -89,6 +89,7 @@ SIGNATURES = {
     "svh_batch_elapsed_ms": (c_int, [c_void_p, P_f32]),
     "svh_batch_plan": (c_int, [c_void_p, c_uint32, POINTER(svh_model_info)]),
     "svh_batch_fallbacks": (c_int, [c_void_p, P_u64]),
+    "svh_batch_debug_fault": (c_int, [c_void_p, c_void_p]),
     "svh_batch_destroy": (c_int, [c_void_p]),
     "svh_viterbi": (c_int, [c_void_p, c_uint32, c_uint64, P_u64, P_u64, P_f32, P_i64, P_i32]),
     "svh_batch_create_u8": (c_int, [c_void_p, c_uint64, P_u64, POINTER(ctypes.c_uint8), c_uint32, POINTER(c_void_p)]),

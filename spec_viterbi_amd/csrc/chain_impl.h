@@ -719,7 +719,7 @@ __global__ __launch_bounds__(64 * W, (GE && W == 4 && SM <= 10 && HA == 1) ? 4 :
         for (int k = 0; k < kBandStamps; ++k)
             m.stamps[((size_t)q * kMaxWaves + wave) * kBandStamps + k] = st_acc[k];
     }
-    if (spins > kSpinLimit && lane == 0 && m.fault) atomicOr(m.fault, 1u);
+    if (spins > kSpinLimit && lane == 0 && b.fault) atomicOr(b.fault, kFaultChain);
 
     // ---- epilogue: scores and the lowest-index argmin ---------------------------------------
     float* out = b.scores + (size_t)q * n;

@@ -44,6 +44,9 @@ struct FusedModel {
     uint32_t B;             // threads per workgroup
 };
 
+// Bits of FusedBatch::fault.
+constexpr uint32_t kFaultPipe = 1u, kFaultPipeWide = 2u, kFaultChain = 4u;
+
 // One batch of sequences.  Symbols are uint8; each sequence 16-byte aligned, kSymPad padded.
 struct FusedBatch {
     const uint8_t* symbols;
@@ -75,6 +78,9 @@ struct FusedBatch {
     // run_mask[q] != 0 run (the others return at once).  Step kernels check it first.
     const uint32_t* run_mask;
     const struct PipeScratch* pipe;  // host side only: scratch of the pipelined kernel (nullable)
+    // The batch's own fault word (nullable): a kernel whose bounded wait gave up ORs its bit in
+    // (kFaultPipe, kFaultPipeWide, kFaultChain); the batch that ran it reports and clears it.
+    uint32_t* fault;
     uint32_t nseq;
 };
 
@@ -117,7 +123,6 @@ struct BandModel {
                    // 4 s_memtime segment stamps into `stamps`, 8 no s_sleep in spins,
                    // 16 chain kernel ignores the exchange tags (never waits)
     unsigned long long* stamps;  // [nseq][kMaxWaves][kBandStamps] cycle sums (dbg & 4)
-    uint32_t* fault;             // chain kernel: set non-zero if a bounded spin gave up
     // decoded paths (chain kernel, HA <= 1):
     const uint8_t* pflags;  // [SM*B] bit0: term from position p-1 exists, bit1: term from heavy
                             // row 0 exists, bit2: heavy row 0 < row of p-1 (heavy wins ties)
@@ -193,7 +198,6 @@ struct PipeModel {
     uint32_t n, S, P, nblk, SM, W, G;  // P = nblk*64*SM positions, G workgroups per sequence
     uint32_t cus;           // wide plan: CUs of the device (W = waves per workgroup at most)
     uint32_t sx;            // S has a term from F
-    uint32_t* fault;        // set non-zero if a bounded wait gave up
     unsigned long long* stamps;  // diagnostics (SVH_PIPE_DEBUG): [ticket][W][8] counters, or null
     uint32_t diag;               // diagnostics with stamps (SVH_PIPE_DEBUG bits > 1): 1 = no boundary
                                  // exchange (every wave runs as block 0; timing only, wrong results)

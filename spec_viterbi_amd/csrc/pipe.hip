@@ -175,11 +175,14 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         };
         uint32_t cwi = first >> 10;
         uint4 cw = load_window(cwi), nw = load_window(cwi + 1);
+        // The wait budget is per window: a new window resets a healthy counter (a give-up sticks),
+        // so no sequence length exhausts it while a stuck wait still gives up within one budget.
         auto window_for = [&](uint32_t t) {  // uniform; windows advance one at a time
             if ((t >> 10) != cwi) {
                 cw = nw;
                 ++cwi;
                 nw = load_window(cwi + 1);
+                spins = spins > kSpinLimit ? spins : 0u;
             }
         };
         auto sym1 = [&](uint32_t t) -> uint32_t {  // symbol of observation t (slow path)
@@ -500,7 +503,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         }
         if (dbg && lane == 0)
             for (int k = 0; k < kPipeStamps; ++k) m.stamps[((size_t)id * W + w) * kPipeStamps + k] = dg[k];
-        if (spins > kSpinLimit && lane == 0 && m.fault) atomicOr(m.fault, 1u);
+        if (spins > kSpinLimit && lane == 0 && b.fault) atomicOr(b.fault, kFaultPipe);
 
         // ---- scores of the light positions and this wave's partials
         float* out = b.scores + (size_t)q * m.n;

@@ -138,11 +138,14 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
         };
         uint32_t cwi = first >> 10;
         uint4 cw = load_window(cwi), nw = load_window(cwi + 1);
+        // The wait budget is per window (as pipe.hip): a new window resets a healthy counter, a
+        // give-up sticks.
         auto window_for = [&](uint32_t t) {
             if ((t >> 10) != cwi) {
                 cw = nw;
                 ++cwi;
                 nw = load_window(cwi + 1);
+                spins = spins > kSpinLimit ? spins : 0u;
             }
         };
         auto sym1 = [&](uint32_t t) -> uint32_t {
@@ -316,6 +319,7 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
                 float bv_prev = bprev;  // lane 7 (all lanes) = boundary of t-1
                 while (t + 32 <= len) {
                   cw = load_window(t >> 10);
+                  spins = spins > kSpinLimit ? spins : 0u;  // new window, new budget
                   // wait for the window here (an asm use of it), so no window load is pending at
                   // the inner loop's header (where the compiler would drain every load)
                   asm volatile("" ::"v"(cw.x), "v"(cw.y), "v"(cw.z), "v"(cw.w));
@@ -417,7 +421,7 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
                 default: sweep(I2{}, I2{}); break;
             }
         }
-        if (spins > kSpinLimit && lane == 0 && m.fault) atomicOr(m.fault, 1u);
+        if (spins > kSpinLimit && lane == 0 && b.fault) atomicOr(b.fault, kFaultPipeWide);
 
         // ---- scores of the light positions, this wave's partials, the sequence's combine
         float* out = b.scores + (size_t)q * m.n;

@@ -814,6 +814,15 @@ void PipeScratchBuffers::ensure(uint32_t rows, uint32_t G, hipStream_t s) {
     view.G = G;
 }
 
+void PipeScratchBuffers::note_launch(hipStream_t s) {
+    if (launches > 0 && launches % kEpochSpan == 0) {
+        hip_check(hipMemsetAsync(d_ctr.ptr, 0, d_ctr.bytes, s), "pipe epoch reset");
+        hip_check(hipMemsetAsync(d_gran.ptr, 0, d_gran.bytes, s), "pipe epoch reset");
+        hip_check(hipMemsetAsync(d_cons.ptr, 0, d_cons.bytes, s), "pipe epoch reset");
+    }
+    ++launches;
+}
+
 void DeviceBandPlan::report_stamps(uint32_t nseq) const {
     if (!(view.dbg & (4u | 128u)) || !view.stamps) return;
     std::vector<unsigned long long> h((size_t)nseq * kMaxWaves * kBandStamps);
@@ -910,12 +919,6 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
             BandPlan wide = make_band_plan(host, 0, true, 4);
             if (wide.ok) band_wide.upload(wide, host.n, host.S, stream);
         }
-        d_faults.alloc(4 * sizeof(uint32_t));
-        hip_check(hipMemsetAsync(d_faults.ptr, 0, d_faults.bytes, stream), "fault words");
-        pipe.view.fault = d_faults.as<uint32_t>() + 0;
-        pipe_wide.view.fault = d_faults.as<uint32_t>() + 1;
-        band.view.fault = d_faults.as<uint32_t>() + 2;
-        band_wide.view.fault = d_faults.as<uint32_t>() + 3;
         int cus = 0;
         hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device), "CU count");
         cu_count = (uint32_t)cus;
@@ -1144,6 +1147,8 @@ void Batch::init(uint32_t flags) {
     DeviceGuard g(model->device);
     hip_check(hipEventCreate(&ev_start), "hipEventCreate");
     hip_check(hipEventCreate(&ev_stop), "hipEventCreate");
+    d_fault.alloc(sizeof(uint32_t));
+    hip_check(hipMemsetAsync(d_fault.ptr, 0, sizeof(uint32_t), model->stream), "fault word");
 }
 
 // (Re)load the batch's sequences: host packing, then asynchronous uploads on `s` into device
@@ -1225,6 +1230,7 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
     }
     spec_ready_level = 0;
     ran = false;
+    pipe_ran = false;
 }
 
 Batch::~Batch() {
@@ -1251,6 +1257,7 @@ void Batch::run(uint32_t level, hipStream_t s) {
     fb.end = d_end.as<uint32_t>();
     fb.scores = d_scores.as<float>();
     fb.best = d_best.as<int64_t>();
+    fb.fault = d_fault.as<uint32_t>();
     fb.nseq = nseq;
     if (paths && chain_paths) {
         fb.cmask = d_cmask.as<uint32_t>();
@@ -1266,6 +1273,7 @@ void Batch::run(uint32_t level, hipStream_t s) {
     pipe_ran = false;
     if (const DevicePipePlan* pp = paths ? nullptr : model->pipe_for(nseq)) {  // pipelined plan: scratch
         pipe.ensure(nseq, pp->plan.G, s);
+        pipe.note_launch(s);
         fb.pipe = &pipe.view;
         pipe_ran = model->band_for(false, nseq) != nullptr;  // launch_steps' condition
     }
@@ -1347,6 +1355,7 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
     if (seg < 2 || probe < 1 || probe >= seg)
         throw Error(SVH_E_INVALID, "time-parallel run needs seg >= 2 and 1 <= probe < seg");
     if (tol != tol) throw Error(SVH_E_INVALID, "tolerance is NaN");  // tol < 0: re-run every segment (exact)
+    pipe_ran = false;  // this pass never uses the pipelined kernel (svh_batch_fallbacks reports 0)
     const uint32_t n = model->host.n;
     struct Seg {
         uint32_t q, k, b, e;
@@ -1430,6 +1439,7 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
         vend.clear();
         const uint8_t* sym = d_sym.as<uint8_t>();
         int64_t* vbest = d_vbest.as<int64_t>();
+        uint32_t* fault = d_fault.as<uint32_t>();
         Model* mdl = model;
         ops.push_back([=](const uint8_t* base) {
             FusedBatch fb;
@@ -1442,6 +1452,7 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
             fb.v_in_row = at32(base, orow);
             fb.scores = out;
             fb.best = vbest;
+            fb.fault = fault;
             fb.nseq = rows;
             mdl->launch_steps(fb, false, s);
         });
@@ -1571,7 +1582,7 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
     if (nflags)
         hip_check(hipMemcpyAsync(flags.data(), d_flag.ptr, (size_t)nflags * 4, hipMemcpyDeviceToHost, s), "flags D2H");
     hip_check(hipStreamSynchronize(s), "time-parallel run");
-    model->check_fault();
+    check_fault(s);
     uint64_t nfall = 0;
     for (uint32_t f : flags) nfall += f;
     if (fallbacks) *fallbacks = nfall;
@@ -1583,19 +1594,19 @@ void Batch::read(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out
     if (!s) s = model->stream;
     if (!ran) throw Error(SVH_E_STATE, "svh_batch_read before svh_batch_run");
     if (paths_out && !paths) throw Error(SVH_E_STATE, "batch was created without SVH_BATCH_PATHS");
-    // scores, best states and the model's fault words into pinned staging on the run's stream,
+    // scores, best states and the batch's fault word into pinned staging on the run's stream,
     // one synchronisation, then out to the caller (pageable copies would each block on their own)
     const size_t sb = scores ? (size_t)nseq * model->host.n * 4 : 0, bb = best ? (size_t)nseq * 8 : 0;
-    const size_t fb = model->d_faults.ptr ? 4 * sizeof(uint32_t) : 0;
+    constexpr size_t fb = 16;  // the fault word, padded (keeps the scores 16-byte aligned)
     uint8_t* st = h_out.reserve(fb + sb + bb);
-    if (fb) hip_check(hipMemcpyAsync(st, model->d_faults.ptr, fb, hipMemcpyDeviceToHost, s), "fault D2H");
+    hip_check(hipMemcpyAsync(st, d_fault.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "fault D2H");
     if (sb) hip_check(hipMemcpyAsync(st + fb, d_scores.ptr, sb, hipMemcpyDeviceToHost, s), "scores D2H");
     if (bb) hip_check(hipMemcpyAsync(st + fb + sb, d_best.ptr, bb, hipMemcpyDeviceToHost, s), "best D2H");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-    if (fb) {
-        uint32_t f[4];
-        std::memcpy(f, st, sizeof(f));
-        model->report_faults(f);
+    {
+        uint32_t f;
+        std::memcpy(&f, st, sizeof(f));
+        report_fault(f, s);
     }
     if (sb) std::memcpy(scores, st + fb, sb);
     if (bb) std::memcpy(best, st + fb + sb, bb);
@@ -1652,20 +1663,30 @@ void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) co
     }
 }
 
-void Model::check_fault() const {
-    if (!d_faults.ptr) return;  // no chain / pipelined plan
-    uint32_t f[4] = {0, 0, 0, 0};
-    hip_check(hipMemcpy(f, d_faults.ptr, sizeof(f), hipMemcpyDeviceToHost), "fault D2H");
-    report_faults(f);
+void Batch::check_fault(hipStream_t s) {
+    DeviceGuard g(model->device);
+    if (!s) s = model->stream;
+    uint32_t* f = reinterpret_cast<uint32_t*>(h_out.reserve(16));
+    hip_check(hipMemcpyAsync(f, d_fault.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "fault D2H");
+    hip_check(hipStreamSynchronize(s), "fault D2H");
+    report_fault(*f, s);
 }
 
-void Model::report_faults(const uint32_t* f) const {
-    if (f[0] | f[1] | f[2] | f[3]) {
-        // reported once: clear the words so the model's later runs are judged on their own
-        hip_check(hipMemset(d_faults.ptr, 0, 4 * sizeof(uint32_t)), "fault reset");
-        if (f[0] | f[1]) throw Error(SVH_E_HIP, "pipelined kernel: a bounded wait gave up (results invalid)");
-        throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
-    }
+void Batch::report_fault(uint32_t f, hipStream_t s) {
+    if (!f) return;
+    // reported once: clear the word (ordered on the stream of the run that set it) so this batch's
+    // later runs are judged on their own; other batches have words of their own
+    hip_check(hipMemsetAsync(d_fault.ptr, 0, sizeof(uint32_t), s), "fault reset");
+    if (f & (kFaultPipe | kFaultPipeWide))
+        throw Error(SVH_E_HIP, "pipelined kernel: a bounded wait gave up (results invalid)");
+    throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
+}
+
+void Batch::inject_fault(hipStream_t s) {
+    DeviceGuard g(model->device);
+    if (!s) s = model->stream;
+    if (!ran) throw Error(SVH_E_STATE, "no run recorded");
+    hip_check(hipMemsetAsync(d_fault.ptr, 0x01, 1, s), "fault inject");  // kFaultPipe
 }
 
 uint64_t Batch::pipe_fallbacks() {

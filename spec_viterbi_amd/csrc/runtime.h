@@ -179,7 +179,13 @@ struct Pinned {
 struct PipeScratchBuffers {
     DeviceBuffer d_ctr, d_done, d_part, d_gran, d_cons, d_viol;
     PipeScratch view{};
+    uint64_t launches = 0;  // pipelined launches on this scratch (its device epoch counts the same)
     void ensure(uint32_t rows, uint32_t G, hipStream_t s);
+    // before every launch: every kEpochSpan launches the granules, progress words and the epoch
+    // counter are re-zeroed on s, so a granule tag (epoch modulo 0xFFFFF, pipe_common.h gtag)
+    // never meets a stale granule of an earlier launch with the same residue
+    void note_launch(hipStream_t s);
+    static constexpr uint64_t kEpochSpan = 1ull << 19;
 };
 
 struct Model {
@@ -204,9 +210,6 @@ struct Model {
     uint32_t spec_level = 0;
     uint32_t pstride = 0;
     DeviceBuffer d_mfold, d_products;
-    // fault words of the bounded waits, one per chain / pipelined plan (pipe, pipe_wide, band,
-    // band_wide): one allocation, so check_fault reads them with a single copy
-    DeviceBuffer d_faults;
 
     Model(const HostModel& h, const svh_model_opts* opts);
     ~Model();
@@ -219,11 +222,6 @@ struct Model {
     const DevicePipePlan* pipe_for(uint32_t nseq) const;
     void spec_build(uint32_t level, hipStream_t s);
     svh_model_info info(uint32_t nseq = 0, bool paths = false, uint32_t level = 0) const;
-    // throws if a bounded wait of a chain / pipelined kernel gave up since the last check
-    // (synchronous; the words are cleared when reported)
-    void check_fault() const;
-    // the same for fault words already copied to the host (f: d_faults' 4 words)
-    void report_faults(const uint32_t* f) const;
     // one pass of the step kernel the model plans for (chain, band, fused or generic)
     void launch_steps(const FusedBatch& b, bool paths, hipStream_t s) const;
 };
@@ -240,6 +238,9 @@ struct Batch {
     bool chain_paths = false;  // paths from the chain kernel's compact records (else fused / generic)
     DeviceBuffer d_cmask, d_cmaskoff, d_hrec, d_hrecoff, d_ckpt, d_ckptoff;
     PipeScratchBuffers pipe;  // pipelined kernel scratch (sized for the rows of each launch)
+    // fault word of this batch's runs (FusedBatch::fault; kFault* bits): only this batch's
+    // kernels write it and only this batch reads and clears it
+    DeviceBuffer d_fault;
     // _spec runs
     DeviceBuffer d_vbuf, d_nchunks, d_tbegin, d_vrow;
     uint32_t spec_ready_level = 0;
@@ -269,9 +270,15 @@ struct Batch {
     void run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream_t s, uint64_t* fallbacks);
     // enqueue result copies (any pointer may be NULL) on s without waiting
     void read_async(hipStream_t s, float* scores, int64_t* best, int32_t* paths);
+    // throws SVH_E_HIP if a bounded wait of this batch's last run gave up (waits on s; the word is
+    // cleared on s when reported, so later runs are judged on their own)
+    void check_fault(hipStream_t s);
+    // diagnostics (svh_batch_debug_fault): mark the last run as if a bounded wait had given up
+    void inject_fault(hipStream_t s);
 
   private:
     void init(uint32_t flags);
+    void report_fault(uint32_t f, hipStream_t s);
 };
 
 }  // namespace svh

@@ -133,7 +133,7 @@ uint64_t decode_file(Model* model, const std::string& path, int format, uint32_t
             hip_check(hipStreamWaitEvent(xs, s.done, 0), "hipStreamWaitEvent");
             b.read_async(xs, sc, be, pa);
             hip_check(hipStreamSynchronize(xs), "results D2H");
-            model->check_fault();
+            b.check_fault(xs);
             decoded += b.nseq;
             return fn(user, s.chunk.first, b.nseq, s.chunk.offsets.data(), sc, be, pa) == 0;
         };

@@ -269,6 +269,13 @@ int svh_batch_fallbacks(svh_batch_t b, uint64_t* rows) {
     });
 }
 
+int svh_batch_debug_fault(svh_batch_t b, void* stream) {
+    return guarded([&] {
+        require(b != nullptr, "null batch");
+        b->impl->inject_fault(static_cast<hipStream_t>(stream));
+    });
+}
+
 int svh_batch_plan(svh_batch_t b, uint32_t level, svh_model_info* info) {
     return guarded([&] {
         require(b && info, "null argument");

@@ -147,6 +147,11 @@ class DeviceBatch:
         _lib.check(_lib.lib.svh_batch_fallbacks(self._h, ctypes.byref(r)))
         return int(r.value)
 
+    def debug_fault(self, stream: int | None = None) -> None:
+        """Diagnostics (svh_batch_debug_fault): mark the last run as if a bounded wait had given
+        up; this batch's next read() raises, other batches of the model are unaffected."""
+        _lib.check(_lib.lib.svh_batch_debug_fault(self._h, ctypes.c_void_p(stream or 0)))
+
     def elapsed_ms(self) -> float:
         ms = ctypes.c_float()
         _lib.check(_lib.lib.svh_batch_elapsed_ms(self._h, ctypes.byref(ms)))

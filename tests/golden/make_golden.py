@@ -4,7 +4,8 @@ The oracle (oracle/viterbi_oracle.c) restates GraphBLAS_impl / GraphBLAS_spec_im
 by the reference's own fixtures (tests/test_helper.h:17-22) -- see tests/test_oracle_golden.py.
 Floats are stored as IEEE-754 bit patterns (hex) so the vectors are exact.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py            # the fixture files below
+    python tests/golden/make_golden.py digests    # score_digests.json (bench workloads)
 """
 from __future__ import annotations
 
@@ -48,7 +49,33 @@ def case(hmm_path, ess_path, seq_ids, levels=(), paths=True):
     return out
 
 
+def digests():
+    """Per-row SHA-256 digests of the exact float32 score bytes (and of the int32 decoded paths)
+    plus best states, for every sequence of the bench workloads: 2405.chmm x emit_50_3500_20
+    (configs[2]) and x covid-19 (configs[4]).  bench.py checks every rank's timed output (and the
+    gathered rows of its strong-scaling modes) against these without running the oracle."""
+    import hashlib
+
+    hmm = svh.read_HMM(os.path.join(DATA, "chmm_files/2405.chmm"))
+    out = {}
+    for ess in ("emit_50_3500_20.ess", "covid-19.ess"):
+        seqs = svh.read_emit_seq(os.path.join(DATA, "ess_files", ess))
+        rows = []
+        for seq in seqs:
+            scores, best, path = oracle.decode(hmm, seq)
+            rows.append({"length": int(seq.size), "best_state": int(best),
+                         "scores_sha256": hashlib.sha256(np.asarray(scores, np.float32).tobytes()).hexdigest(),
+                         "path_sha256": hashlib.sha256(np.asarray(path, np.int32).tobytes()).hexdigest()})
+        out[f"2405.chmm x {ess}"] = rows
+        print("digests", ess, len(rows))
+    with open(os.path.join(OUT, "score_digests.json"), "w") as f:
+        json.dump(out, f, indent=0)
+
+
 def main():
+    if sys.argv[1:] == ["digests"]:
+        digests()
+        return
     goldens = {
         "test_chmms": [case(f"chmm_files/test_chmms/{i}_test_chmm.chmm", f"ess_files/test_sequences/{i}_test_seq.ess",
                             range(2 if i == 0 else 1), levels=(1, 2, 3)) for i in range(4)],

@@ -80,9 +80,13 @@ def test_2405_emit50_full_batch_vs_oracle():
     hmm = svh.read_HMM(chmm("2405.chmm"))
     seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
     model = svh.DeviceModel(hmm)
-    info = model.info()
-    assert info["kernel"] == _lib.SVH_KERNEL_CHAIN and info["heavy_uniform"] == 1, info
-    scores, best = model.viterbi(seqs)
+    batch = model.batch(seqs)
+    plan = batch.plan()
+    # AUTO takes the pipelined latency plan for this batch (50 sequences x 5 workgroups)
+    assert plan["kernel"] == _lib.SVH_KERNEL_PIPE and plan["pipe_groups"] == 5, plan
+    batch.run()
+    scores, best = batch.read()
+    assert batch.fallbacks() == 0
     ref, _ = oracle.viterbi_batch(hmm, seqs, nthreads=16)
     for q in range(len(seqs)):
         assert bit_equal(scores[q], ref[q]), (q, first_mismatch(scores[q], ref[q]))
@@ -351,19 +355,24 @@ def test_wide_batch_streamed_plan_2405():
 
 def test_chain_long_sequence_no_fault():
     """A 10 M-observation sequence on 8 waves of the chain kernel (the most inter-wave waits per
-    observation): every bounded wait is per wait, so length alone never trips the fault word
-    (round-1 budget was cumulative per sequence).  Scores bit-exact against the oracle."""
+    observation): the wait budget is reset per symbol chunk, so length alone never trips the fault
+    word (round-1 budget was cumulative per sequence).  The chain kernel is forced and the batch's
+    own plan asserted (AUTO would pick the one-wave pipelined plan, which never waits).  Scores
+    bit-exact against the oracle."""
     hmm = svh.read_HMM(chmm("100.chmm"))
     rng = np.random.default_rng(7)
     seq = rng.integers(0, hmm.emit_num, size=10_000_000).astype(np.uint64)
     os.environ["SVH_CHAIN_WAVES"] = "8"
     try:
-        model = svh.DeviceModel(hmm)
+        model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_CHAIN)
     finally:
         os.environ.pop("SVH_CHAIN_WAVES", None)
-    info = model.info()
-    assert info["kernel"] == _lib.SVH_KERNEL_CHAIN and info["threads"] == 512, info
-    got, best = model.viterbi([seq])
+    batch = model.batch([seq])
+    plan = batch.plan()
+    assert plan["kernel"] == _lib.SVH_KERNEL_CHAIN and plan["threads"] == 512, plan
+    batch.run()
+    got, best = batch.read()
+    batch.close()
     ref = oracle.viterbi(hmm, seq)
     assert bit_equal(got[0], ref), first_mismatch(got[0], ref)
     # and the model stays usable (no stale fault) on a second run

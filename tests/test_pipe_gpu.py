@@ -270,20 +270,26 @@ def test_pipew_other_pfam_models_replicated(name):
     assert_same(s, b, sc, bc)
 
 
-def test_pipe_spec3_tail_starting_at_256():
+@pipes
+def test_pipe_spec3_tail_starting_at_256(kern):
     """Regression for the pipelined kernels' initial progress word: a `_spec`
     level-3 tail that starts at observation 256 (a multiple of 64 past the flow-control window)
-    and runs two observations, on a latency plan with two workgroups per sequence.  Before the
-    fix the producer's first flow-control wait and the consumer's first granule wait deadlocked
-    (a bounded-wait give-up).  Checked bit-exact against the serial chain kernel at level 3 and
-    within the reference's tolerance of the non-spec oracle."""
+    and runs two observations, on a plan with two workgroups (latency plan) or two position blocks
+    (wide plan) per sequence.  Before the fix the producer's first flow-control wait and the
+    consumer's first granule wait deadlocked (a bounded-wait give-up).  Checked bit-exact against
+    the serial chain kernel at level 3 and within the reference's tolerance of the non-spec
+    oracle."""
     hmm = svh.read_HMM(chmm("1001.chmm"))
     seq = svh.read_emit_seq(ess("emit_3_3500_20.ess"))[0][:258]
-    model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_PIPE)
+    model = svh.DeviceModel(hmm, kernel=kern)
     info = model.info()
-    assert info["pipe_groups"] >= 2, info
+    assert (info["pipe_groups"] if kern == _lib.SVH_KERNEL_PIPE else info["pipew_blocks"]) >= 2, info
     model.spec_build(3)
-    got, _ = model.viterbi([seq], level=3)
+    batch = model.batch([seq])
+    assert batch.plan(3)["kernel"] == kern
+    batch.run(3)
+    got, _ = batch.read()
+    batch.close()
     model.close()
     chain = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_CHAIN)
     chain.spec_build(3)
@@ -291,3 +297,81 @@ def test_pipe_spec3_tail_starting_at_256():
     chain.close()
     assert bit_equal(got[0], ref[0]), first_mismatch(got[0], ref[0])
     assert all(svh.almost_equal(a, b) for a, b in zip(got[0], oracle.viterbi(hmm, seq)))
+
+
+@pipes
+def test_pipe_10M_observations_multi_block_no_fault(kern):
+    """A 10 M-observation sequence on a model of 2,400 light states (5 workgroups of the latency
+    plan, 5 position blocks of the wide plan: 4 boundary exchanges per observation), so it meets
+    millions of slow-path re-reads.  The wait budget is reset per 1,024-observation symbol window
+    (a give-up sticks), so length alone never trips the fault word.  Bit-exact against the serial
+    chain kernel, no fallback row, and the model and batch stay usable afterwards."""
+    hmm = random_chain_hmm(2400, S=20, seed=41, n_from_m=False)
+    seqs = random_seqs(20, [10_000_000], seed=42)
+    model = svh.DeviceModel(hmm, kernel=kern)
+    batch = model.batch(seqs)
+    plan = batch.plan()
+    assert plan["kernel"] == kern
+    assert (plan["pipe_groups"] if kern == _lib.SVH_KERNEL_PIPE else plan["pipew_blocks"]) >= 4, plan
+    batch.run()
+    s, b = batch.read()
+    assert batch.fallbacks() == 0
+    batch.close()
+    sc, bc, _, _ = run(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN)
+    assert_same(s, b, sc, bc)
+    short = random_seqs(20, [3000], seed=43)
+    s2, b2 = model.viterbi(short)
+    oracle_check(hmm, short, s2, b2)
+    model.close()
+
+
+def test_fault_words_are_per_batch():
+    """Two batches of one model on two streams; one is marked as if its bounded wait gave up
+    (svh_batch_debug_fault).  Only that batch's read fails, once; the other batch's reads, before
+    and after, succeed with correct scores, and the failed batch is judged on its own next run."""
+    import torch
+
+    hmm = random_chain_hmm(900, S=20, seed=51, n_from_m=False)
+    model = svh.DeviceModel(hmm)
+    seqs_a, seqs_b = random_seqs(20, [700, 33], seed=52), random_seqs(20, [100, 2000], seed=53)
+    a, b = model.batch(seqs_a), model.batch(seqs_b)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    a.run(0, sa.cuda_stream)
+    b.run(0, sb.cuda_stream)
+    b.debug_fault(sb.cuda_stream)
+    ra = a.read(sa.cuda_stream)  # A must not see (or clear) B's fault
+    oracle_check(hmm, seqs_a, *ra)
+    with pytest.raises(_lib.SvhError):
+        b.read(sb.cuda_stream)
+    ra2 = a.read(sa.cuda_stream)
+    oracle_check(hmm, seqs_a, *ra2)
+    b.run(0, sb.cuda_stream)  # reported once: the next run of B is judged on its own
+    rb = b.read(sb.cuda_stream)
+    oracle_check(hmm, seqs_b, *rb)
+    a.close()
+    b.close()
+    model.close()
+
+
+def test_fallbacks_reset_by_time_parallel_run():
+    """svh_batch_fallbacks reports the last run only: after a pipelined run() with fallback rows,
+    a time-parallel pass (which never uses the pipelined kernel) reports 0."""
+    for seed in range(6):  # the seeds of test_pipe_fallback_rows_match_oracle: some fall back
+        hmm = random_chain_hmm(300, S=8, seed=seed)
+        rows, cols = hmm.trans_rows.astype(np.int64), hmm.trans_cols.astype(np.int64)
+        probs = hmm.trans_probs.copy()
+        probs[(cols == 0) & (rows != 0)] = np.float32(0.0)
+        hmm.trans_probs = probs
+        model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_PIPE)
+        batch = model.batch(random_seqs(8, [700, 1, 40, 333], seed=seed))
+        batch.run()
+        batch.read()
+        if batch.fallbacks() > 0:
+            break
+        batch.close()
+        model.close()
+    assert batch.fallbacks() > 0
+    batch.run_time_parallel(seg_len=128, probe_len=16, rel_tol=-1.0)
+    assert batch.fallbacks() == 0
+    batch.close()
+    model.close()

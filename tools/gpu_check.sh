@@ -4,10 +4,11 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
+TAG=${TAG:-r03}
 mkdir -p gpurun_out
-timeout -k 10 420 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 &&
-timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 &&
-bash tools/profile.sh
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_${TAG}.log 2>&1 &&
+timeout -k 10 300 python bench.py > gpurun_out/bench_${TAG}.log 2>&1 &&
+TAG=$TAG bash tools/profile.sh
 rc=$?
-tail -3 gpurun_out/pytest_gpu.log; tail -2 gpurun_out/bench.log
+tail -3 gpurun_out/pytest_gpu_${TAG}.log; tail -2 gpurun_out/bench_${TAG}.log
 exit $rc
