@@ -104,6 +104,7 @@ __global__ __launch_bounds__(64) void chain_traceback_kernel(BandModel m, FusedB
                                                               int32_t* paths) {
     __shared__ float buf[2 * kTbMaxCap];
     const uint32_t q = blockIdx.x, lane = threadIdx.x;
+    if (b.run_mask && !b.run_mask[q]) return;  // rows the pipelined kernel traced itself
     const uint32_t len = b.end[q];
     const uint32_t SM = m.SM, B = m.B;
     const uint32_t* msk = b.cmask + b.cmask_off[q];

@@ -140,5 +140,27 @@ __device__ __forceinline__ void lds_dma16(const void* gsrc, uint32_t lds_base_un
         : "memory");
 }
 
+// acc = (acc << 1) | bit per lane as v_addc_co_u32 acc, acc, acc with the compare's lane mask in
+// VCC as the carry-in (hipcc's own code for the same C is four VALU ops: compare, shift, select,
+// or).  push_le: bit = [x <= y]; push_lt_eqc: bit = [x < y] | (c & [x == y]), c a lane mask.
+__device__ __forceinline__ void push_le(uint32_t& acc, float x, float y) {
+    asm volatile("v_cmp_le_f32_e32 vcc, %1, %2\n\t"
+                 "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                 : "+v"(acc)
+                 : "v"(x), "v"(y)
+                 : "vcc");
+}
+__device__ __forceinline__ void push_lt_eqc(uint32_t& acc, float x, float y, uint64_t c) {
+    uint64_t e;
+    asm volatile("v_cmp_eq_f32_e64 %1, %2, %3\n\t"
+                 "s_and_b64 %1, %1, %4\n\t"
+                 "v_cmp_lt_f32_e32 vcc, %2, %3\n\t"
+                 "s_or_b64 vcc, vcc, %1\n\t"
+                 "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                 : "+v"(acc), "=&s"(e)
+                 : "v"(x), "v"(y), "s"(c)
+                 : "vcc", "scc");
+}
+
 }  // namespace dev
 }  // namespace svh

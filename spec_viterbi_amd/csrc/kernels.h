@@ -74,6 +74,16 @@ struct FusedBatch {
     const uint64_t* hrec_off;   // [nseq] u32 offset of sequence q's records
     float* ckpt;
     const uint64_t* ckpt_off;   // [nseq] float offset of sequence q's checkpoint rows
+    // Pipelined-kernel decoded paths (pipe.hip PATHS, pipe_paths.hip): cmask / ckpt / hrec above
+    // in the pipelined plan's layouts (kernels.h, PipeModel), plus
+    //   prec: [blk][half][t] per-block partial records {min of the half-wave's light scores at
+    //         t-1, min of its sink partials at t} for observations t in [1, len); the traceback
+    //         kernel folds them into hrec rows {F, C, mu}
+    //   fck:  F's score at every 32nd observation (F(32k)), written by block 0
+    float2* prec;
+    const uint64_t* prec_off;   // [nseq] float2 offset of sequence q's partial records
+    float* fck;
+    const uint64_t* fck_off;    // [nseq] float offset of sequence q's F checkpoints
     // Fallback pass after the pipelined kernel (pipe.hip): when set, only rows with
     // run_mask[q] != 0 run (the others return at once).  Step kernels check it first.
     const uint32_t* run_mask;
@@ -198,6 +208,13 @@ struct PipeModel {
     uint32_t n, S, P, nblk, SM, W, G;  // P = nblk*64*SM positions, G workgroups per sequence
     uint32_t cus;           // wide plan: CUs of the device (W = waves per workgroup at most)
     uint32_t sx;            // S has a term from F
+    // decoded paths (pipe PATHS variant + pipe_traceback_kernel):
+    const uint8_t* pflags;  // [P] bit0: term from position p-1 exists, bit1: term from F exists,
+                            // bit2: F's row < row of p-1 (F wins ties)
+    const int32_t* spos;    // [n] position of a light row, -1 for F, -2 for S
+    uint32_t hx_exist;      // BandModel::hx_exist (heavy x: 0 = F, 1 = S)
+    uint32_t hl_exist;      // BandModel::hl_exist
+    uint32_t ties_heavy;    // every light position with an F term has it win ties
     unsigned long long* stamps;  // diagnostics (SVH_PIPE_DEBUG): [ticket][W][8] counters, or null
     uint32_t diag;               // diagnostics with stamps (SVH_PIPE_DEBUG bits > 1): 1 = no boundary
                                  // exchange (every wave runs as block 0; timing only, wrong results)
@@ -213,12 +230,29 @@ struct PipeScratch {
     uint32_t* viol;   // [rows] 1: speculation failed, row needs the serial kernel
     uint32_t rows, G;
 };
-inline size_t pipe_lds_bytes(uint32_t W, uint32_t S) {
+__host__ __device__ inline size_t pipe_lds_bytes(uint32_t W, uint32_t S) {
     // boundary ring [W][kPipeRing][64] | counters [16] | heavy constants [S][8] | reduction [W][4] | ticket
     return ((size_t)W * kPipeRing * 64 + 16 + (size_t)S * 8 + (size_t)W * 4 + 4) * 4;
 }
 bool pipe_supported(int sm, int waves, bool sx);
+// b.cmask != nullptr selects the decoded-path variant (every sequence must start at step 0).
 hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
+bool pipe_paths_supported(int sm, int waves);
+// Decoded paths of the pipelined plan: the records {F, C, mu} from the per-block partials, then
+// the path walk (pipe_paths.hip); rows with skip[q] != 0 (re-run by the chain kernel) are left
+// to the chain traceback.
+hipError_t launch_pipe_traceback(const PipeModel& m, const FusedBatch& b, const uint64_t* path_off, int32_t* paths,
+                                 const uint32_t* skip, hipStream_t stream);
+// Per-sequence sizes of the decoded-path buffers of the pipelined plan.
+inline uint64_t pipe_mask_words(uint64_t len, uint32_t nblk, uint32_t sm) {
+    return len > 1 ? (len - 1 + 31) / 32 * (uint64_t)nblk * sm * 64 : 0;
+}
+inline uint64_t pipe_prec_count(uint64_t len, uint32_t nblk) { return (uint64_t)nblk * 2 * len; }
+inline uint64_t pipe_ckpt_floats(uint64_t len, uint32_t P) { return len ? ((len - 1) / kCkptEvery + 1) * (uint64_t)P : 0; }
+inline uint64_t pipe_fck_floats(uint64_t len) { return len ? (len - 1) / 32 + 1 : 0; }
+// LDS of the decoded-path variant beyond pipe_lds_bytes: a ring of 32 rows {pm, c} per wave
+constexpr uint32_t kPRingStride = 132;  // floats per row: 64 lanes x 2 + 4 padding (bank spread)
+inline size_t pipe_path_lds_bytes(uint32_t W) { return (size_t)W * 32 * kPRingStride * 4; }
 // Wide pipelined plan (pipe_wide.hip): one block of 64*SM positions per workgroup, W sequences
 // (one per wave), the block's table [nblk][S][NC][64] float4 in LDS (PipeModel.tab; G = nblk);
 // NC = SM/2 (eb|ea) chunks + {A_S A_F X_SS X_FF} [+ {X_SF 0 0 0} when sx], constants per lane.

@@ -27,6 +27,14 @@
 // fl(a + .) is monotone), F' = fl(X_FF + F), and the check fl(A_F + m) < F' (a violation: F
 // would have taken its light term, the speculation and everything after it is void).
 // The last workgroup of a sequence to finish combines the partials (S, argmin, violation).
+//
+// Decoded paths (PATHS = 1, 2): per observation and light position the "took F's term" bit
+// (compare into VCC + v_addc into a per-lane word per slot, stored every 32 observations; PATHS 2
+// when F wins every tie: one compare), per observation the lane's {light minimum of t-1, sink
+// partial of t} into an LDS ring that the wave folds every 32 observations into per-half-wave
+// partial records (transposed: lane l reduces row l % 32 over its half), light-score checkpoints
+// every kCkptEvery observations and F every 32 (block 0).  pipe_paths.hip turns these into the
+// heavy records and walks the paths.
 #include "pipe_common.h"
 
 namespace svh {
@@ -89,7 +97,7 @@ __device__ __forceinline__ void chain_terms_v(float& xb, float& xa, float eb, fl
     }
 }
 
-template <int SM, int W, bool SX>
+template <int SM, int W, bool SX, int PATHS>
 __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* ring = lds;                                                  // [W][kR][64]
@@ -97,6 +105,8 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     float* ctab = reinterpret_cast<float*>(cnt + 16);                   // [S][8]
     float* red = ctab + m.S * 8;                                        // [W][4]
     uint32_t* tick = reinterpret_cast<uint32_t*>(red + W * 4);
+    // PATHS: [W][32][kPRingStride] rows {pm, c} per lane, 16-byte aligned after the rest
+    float* pring = lds + (pipe_lds_bytes(W, m.S) + 15) / 16 * 4;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t w = (uint32_t)uniform((int)(tid >> 6));
@@ -125,6 +135,11 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     f2 CF;        // {S partial of this lane, F'} (one register pair: the packed heavy update)
     uint64_t viol = 0;
     uint32_t spins = 0;
+    // PATHS: the last 32 "took F's term" bits per slot (bit 0 = newest), the static tie masks
+    // (PATHS 1), the lane's light minimum of the last step's input scores
+    uint32_t macc[PATHS ? SM : 1] = {};
+    uint64_t pmC[PATHS ? SM : 1] = {};
+    float last_pm = kInf;
     // diagnostics: 0 loop cycles, 1 head cycles, 2 tail cycles, 3 slow re-reads waiting for the
     // previous wave, 4 ... for the next wave (flow control), 5 ... for granules, 6 ... for the
     // consumer's progress word, 7 body iterations
@@ -167,6 +182,81 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             CF.x = (blk == 0 && lane == 0 && m.rowS >= 0) ? vin[m.rowS] : kInf;
         }
 
+        // ---- decoded paths: outputs and the per-slot tie masks
+        float* const pring_w = pring + w * 32 * kPRingStride;
+        uint32_t* const cmq = PATHS ? b.cmask + b.cmask_off[q] : nullptr;
+        float* const ckq = PATHS ? b.ckpt + b.ckpt_off[q] : nullptr;
+        float2* const precq = PATHS ? b.prec + b.prec_off[q] : nullptr;
+        float* const fckq = PATHS ? b.fck + b.fck_off[q] : nullptr;
+        const uint32_t wstride = m.nblk * SM * 64;  // mask words per 32 rows
+        auto store_masks = [&](uint32_t word, uint32_t rows) {  // rows 32*word .. +rows-1 are in macc
+#pragma unroll
+            for (int s = 0; s < SM; ++s)
+                cmq[(size_t)word * wstride + (blk * SM + s) * 64 + lane] = macc[s] << (32u - rows);
+        };
+        auto checkpoint = [&](uint32_t t) {  // t % kCkptEvery == 0: the light scores of t
+            float* d = ckq + (size_t)(t / kCkptEvery) * m.P + p0;
+            if constexpr (SM == 2) {
+                *reinterpret_cast<float2*>(d) = make_float2(v[0], v[1]);
+            } else {
+#pragma unroll
+                for (int s = 0; s < SM; ++s) d[s] = v[s];
+            }
+        };
+        auto ring_put2 = [&](uint32_t t) {  // {light minimum of t-1, sink partial of t}
+            *reinterpret_cast<float2*>(pring_w + (t & 31u) * kPRingStride + lane * 2) = make_float2(last_pm, CF.x);
+        };
+        // fold rows tb .. tb+31 of the ring (tb % 32 == 0) and store observations t in [1, thi):
+        // lane l reduces row l % 32 over the half-wave l / 32 (conflict-free: rows 528 B apart)
+        auto reduce_ring = [&](uint32_t tb, uint32_t thi) {
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const uint32_t R = lane & 31u, H = lane >> 5;
+            const float4* rp = reinterpret_cast<const float4*>(pring_w + R * kPRingStride + H * 64);
+            float mm = kInf, cc = kInf;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float4 e = rp[i];
+                mm = fminf(mm, fminf(e.x, e.z));
+                cc = fminf(cc, fminf(e.y, e.w));
+            }
+            const uint32_t tt = tb + R;
+            if (tt >= 1 && tt < thi) precq[((size_t)blk * 2 + H) * len + tt] = make_float2(mm, cc);
+        };
+        // after the step of observation t (compile-time positions in the unrolled body)
+        auto paths_after = [&](uint32_t t, auto maskc, auto ckc, auto redc) {
+            if constexpr (PATHS) {
+                ring_put2(t);
+                if constexpr (decltype(maskc)::value) {
+                    if (t >= 32) store_masks((t >> 5) - 1, 32);
+                    if (blk == 0 && lane == 0) fckq[t >> 5] = CF.y;
+                }
+                if constexpr (decltype(ckc)::value) checkpoint(t);
+                if constexpr (decltype(redc)::value) reduce_ring(t - 31, len);
+            }
+        };
+        auto paths_after_rt = [&](uint32_t t) {  // runtime positions (head / tail)
+            if constexpr (PATHS) {
+                ring_put2(t);
+                if ((t & 31u) == 0) {
+                    if (t >= 32) store_masks((t >> 5) - 1, 32);
+                    if (blk == 0 && lane == 0) fckq[t >> 5] = CF.y;
+                }
+                if ((t & (kCkptEvery - 1)) == 0) checkpoint(t);
+                if ((t & 31u) == 31u) reduce_ring(t - 31, len);
+            }
+        };
+        if constexpr (PATHS) {
+#pragma unroll
+            for (int s = 0; s < SM; ++s) {
+                const uint32_t f = m.pflags[p0 + s];
+                const bool ec = f & 1u, eaf = f & 2u, hl = f & 4u;
+                pmC[s] = __builtin_amdgcn_ballot_w64(eaf && (!ec || hl));
+            }
+            checkpoint(0);
+            if (blk == 0 && lane == 0) fckq[0] = CF.y;
+        }
+
         // ---- symbols: 1024-observation windows in VGPRs (lane l: bytes 16l..16l+15)
         const uint32_t slen = len + kSymPad;
         auto load_window = [&](uint32_t wi) -> uint4 {
@@ -205,17 +295,27 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 #pragma unroll
             for (int s = 0; s < SM; ++s) asm volatile("" : "+v"(eb[s]), "+v"(ea[s]));  // one idx block
             float vn[SM];
+            auto push = [&](int s, float xa, float xb) {  // PATHS: F's term taken (row t-1's bit)
+                if constexpr (PATHS == 2) push_le(macc[s], xa, xb);
+                else if constexpr (PATHS == 1) push_lt_eqc(macc[s], xa, xb, pmC[s]);
+            };
             {
                 float xb, xa;
                 chain(xb, xa, eb[0], ea[0], CF.y, v[SM - 1]);
                 vn[0] = fminf(xa, xb);
+                if constexpr (PATHS) push(0, xa, xb);
             }
 #pragma unroll
-            for (int s = 1; s < SM; ++s) vn[s] = fminf(ea[s] + CF.y, eb[s] + v[s - 1]);
+            for (int s = 1; s < SM; ++s) {
+                const float xa = ea[s] + CF.y, xb = eb[s] + v[s - 1];
+                vn[s] = fminf(xa, xb);
+                if constexpr (PATHS) push(s, xa, xb);
+            }
             // heavy side from the scores of t-1
             float pm = v[0];
 #pragma unroll
             for (int s = 1; s < SM; ++s) pm = fminf(pm, v[s]);
+            if constexpr (PATHS) last_pm = pm;
             const f2 s1 = (f2){kas, kaf} + (f2){pm, pm};  // A_S + m, A_F + m
             const f2 s2 = (f2){kxss, kxff} + CF;          // X_SS + c, X_FF + F
             float cn = fminf(s1.x, s2.x);
@@ -308,6 +408,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 });
                 ring_put(t, v[SM - 1]);
                 if constexpr (DST == 2) put_gran1(t, readlane_f(v[SM - 1], 63));
+                paths_after_rt(t);
                 if (t + 1 < len) {  // fetch the boundary score of t for the next step
                     if constexpr (SRC == 1) {
                         wait_prev(t + 1);
@@ -426,6 +527,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                 });
                             }
                             ring_w[(8 * j + k) * 64 + lane] = v[SM - 1];
+                            paths_after(tg + k, std::bool_constant<j == 0 && k == 0>{},
+                                        std::bool_constant<k == 0 && (j == 0 || j == 2)>{},
+                                        std::bool_constant<j == 3 && k == 7>{});
                             if constexpr (k == 4) {  // the counts checked at the end of the group
                                 asm volatile("" ::: "memory");
                                 if constexpr (SRC == 1) pc_rd = lds_ld32(cnt_w - 1);
@@ -481,6 +585,13 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             // tail
             for (; t < len; ++t) single(t);
             if (dbg) dg[2] = __builtin_amdgcn_s_memtime() - c0;
+            if constexpr (PATHS) {
+                // rows the loop did not store: masks of rows below len-1 past the last full word,
+                // ring rows of the last partial group of 32
+                const uint32_t mdone = (len - 1) & ~31u;
+                if (mdone < len - 1) store_masks(mdone >> 5, len - 1 - mdone);
+                if (((len - 1) & 31u) != 31u) reduce_ring((len - 1) & ~31u, len);
+            }
         };
 
         if (len > first && dbg && (m.diag & 1u)) {
@@ -586,10 +697,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     }
 }
 
-template <int SM, int W>
+template <int SM, int W, int PATHS = 0>
 const void* pipe_ptr(bool sx) {
-    return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<SM, W, true>)
-              : reinterpret_cast<const void*>(&pipe_viterbi_kernel<SM, W, false>);
+    return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<SM, W, true, PATHS>)
+              : reinterpret_cast<const void*>(&pipe_viterbi_kernel<SM, W, false, PATHS>);
 }
 
 const void* pipe_fn(int sm, int waves, bool sx) {
@@ -602,15 +713,25 @@ const void* pipe_fn(int sm, int waves, bool sx) {
     }
 }
 
+// decoded-path variant: the default geometry only (2 slots, 4 waves)
+const void* pipe_paths_fn(int sm, int waves, bool sx, bool ties_heavy) {
+    if (sm != 2 || waves != 4) return nullptr;
+    return ties_heavy ? pipe_ptr<2, 4, 2>(sx) : pipe_ptr<2, 4, 1>(sx);
+}
+
 }  // namespace
 
 bool pipe_supported(int sm, int waves, bool sx) { return pipe_fn(sm, waves, sx) != nullptr; }
+bool pipe_paths_supported(int sm, int waves) { return pipe_paths_fn(sm, waves, false, false) != nullptr; }
 
 hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream) {
-    const void* fn = pipe_fn((int)m.SM, (int)m.W, m.sx != 0);
+    const bool paths = b.cmask != nullptr;
+    const void* fn = paths ? pipe_paths_fn((int)m.SM, (int)m.W, m.sx != 0, m.ties_heavy != 0)
+                           : pipe_fn((int)m.SM, (int)m.W, m.sx != 0);
     if (!fn || m.S > 32 || m.G == 0 || m.nblk > m.G * m.W || m.P != m.nblk * 64 * m.SM || !x.ctr ||
         b.nseq > x.rows || x.G < m.G)
         return hipErrorInvalidValue;
+    if (paths && (!b.ckpt || !b.prec || !b.fck || !m.pflags)) return hipErrorInvalidValue;
     if (b.nseq == 0) return hipSuccess;
     PipeModel mm = m;
     FusedBatch bb = b;
@@ -618,7 +739,13 @@ hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratc
     void* args[] = {&mm, &bb, &xx};
     const uint64_t grid = (uint64_t)b.nseq * m.G;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    return hipLaunchKernel(fn, dim3((uint32_t)grid), dim3(64 * m.W), args, pipe_lds_bytes(m.W, m.S), stream);
+    const size_t lds = paths ? (pipe_lds_bytes(m.W, m.S) + 15) / 16 * 16 + pipe_path_lds_bytes(m.W)
+                             : pipe_lds_bytes(m.W, m.S);
+    if (lds > 64 * 1024) {  // more than 64 KiB of dynamic LDS: a host-side attribute of the function
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    return hipLaunchKernel(fn, dim3((uint32_t)grid), dim3(64 * m.W), args, lds, stream);
 }
 
 }  // namespace svh

@@ -698,6 +698,22 @@ PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm, uint32_t waves, bool w
             }
         }
     }
+    // decoded paths: term flags per position (as BandPlan::pflags with heavy feeder F) and the
+    // state -> position map (-1 F, -2 S)
+    pp.pflags.assign(P, 0);
+    pp.spos.assign(n, 0);
+    pp.ties_heavy = nL > 0;
+    for (uint32_t p = 0; p < nL; ++p) {
+        uint8_t f = sh.bex[p] ? 1 : 0;
+        if (sh.aex[0][p]) f |= 2;
+        if (p > 0 && sh.heavy[0] < sh.light[p - 1]) f |= 4;
+        pp.pflags[p] = f;
+        pp.ties_heavy = pp.ties_heavy && (f & 2) && (!(f & 1) || (f & 4));
+        pp.spos[sh.light[p]] = (int32_t)p;
+    }
+    for (uint32_t x = 0; x < H; ++x) pp.spos[sh.heavy[x]] = -1 - (int32_t)x;
+    pp.hx_exist = sh.hx_exist;
+    pp.hl_exist = sh.hl_exist;
     pp.hc.assign((size_t)S * 8, kInfH);
     auto wide_consts = [&](uint32_t o, const float* c) {  // wide: constants chunk(s) of every lane
         for (uint32_t blk = 0; blk < pp.nblk; ++blk)
@@ -737,7 +753,14 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     d_start.upload(p.start.data(), p.start.size() * 4, s);
     d_lrow.upload(p.lrow.data(), p.lrow.size() * 4, s);
     d_hc.upload(p.hc.data(), p.hc.size() * 4, s);
+    d_pflags.upload(p.pflags.data(), p.pflags.size(), s);
+    d_spos.upload(p.spos.data(), p.spos.size() * 4, s);
     std::memset(&view, 0, sizeof(view));
+    view.pflags = d_pflags.as<uint8_t>();
+    view.spos = d_spos.as<int32_t>();
+    view.hx_exist = p.hx_exist;
+    view.hl_exist = p.hl_exist;
+    view.ties_heavy = p.ties_heavy ? 1u : 0u;
     view.tab = d_tab.as<float2>();
     view.e0 = d_e0.as<float>();
     view.start = d_start.as<float>();
@@ -1010,6 +1033,15 @@ const DevicePipePlan* Model::pipe_for(uint32_t nseq) const {
     return nullptr;
 }
 
+const DevicePipePlan* Model::pipe_paths_for(uint32_t nseq) const {
+    if (!pipe.plan.ok || !pipe_paths_supported((int)pipe.plan.SM, (int)pipe.plan.W) || pipe.plan.P > 2560 ||
+        !band.plan.paths_ok())
+        return nullptr;
+    if (kernel_pref == SVH_KERNEL_PIPE) return &pipe;
+    if (kernel_pref == SVH_KERNEL_AUTO && nseq <= pipe_max_nseq) return &pipe;
+    return nullptr;
+}
+
 const DevicePlan* Model::plan_for(bool paths) const {
     if (kernel_pref == SVH_KERNEL_GENERIC) return nullptr;
     const DevicePlan* p = paths ? paths_plan : &fast_plan;
@@ -1070,8 +1102,9 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
     const DevicePlan* p = plan_for(paths && steps);
     const DeviceBandPlan* bpl = band_for(paths && steps, nseq);
     i.kernel = bpl ? (bpl->plan.chain ? SVH_KERNEL_CHAIN : SVH_KERNEL_BAND) : p ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
-    // the pipelined plan runs scores-only passes and the step-kernel tail of _spec level >= 2
-    const DevicePipePlan* ppl = !paths && nseq ? pipe_for(nseq) : nullptr;
+    // the pipelined plan runs scores-only passes, the step-kernel tail of _spec level >= 2 and
+    // (latency plan) decoded-path passes of small batches
+    const DevicePipePlan* ppl = !nseq ? nullptr : !paths ? pipe_for(nseq) : steps ? pipe_paths_for(nseq) : nullptr;
     i.family = p ? p->plan.family : -1;
     i.threads = p ? (int32_t)p->plan.B : (int32_t)std::min<uint32_t>(1024, round_up(host.n, 64));
     i.slots = p ? (int32_t)p->plan.SM : 0;
@@ -1093,7 +1126,8 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
     }
     i.spec_level = spec_level;
     i.spec_bytes = d_products.bytes;
-    i.paths_kernel = band_for(true) ? SVH_KERNEL_CHAIN : plan_for(true) ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
+    i.paths_kernel = pipe_paths_for(1) ? SVH_KERNEL_PIPE
+                     : band_for(true) ? SVH_KERNEL_CHAIN : plan_for(true) ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
     i.wide_threads = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.B : 0;
     i.wide_slots = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.SM : 0;
     i.cu_count = cu_count;
@@ -1161,6 +1195,8 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
     if (!offs || (!sym64 && !sym8)) throw Error(SVH_E_INVALID, "null offsets/symbols");
     const DeviceBandPlan* cpl = chain_paths ? model->band_for(true) : nullptr;
     nseq = (uint32_t)nseq_;
+    const DevicePipePlan* ppl = chain_paths ? model->pipe_paths_for(nseq) : nullptr;
+    pipe_paths = ppl != nullptr;
     offsets.assign(offs, offs + nseq + 1);
     lens.resize(nseq);
     h_symoff.resize(nseq);
@@ -1169,7 +1205,11 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
     h_cmoff.resize(nseq);
     h_hroff.resize(nseq);
     h_ckoff.resize(nseq);
-    uint64_t bytes = 0, bpn = 0, cmn = 0, hrn = 0, ckn = 0;
+    h_pmoff.resize(pipe_paths ? nseq : 0);
+    h_proff.resize(pipe_paths ? nseq : 0);
+    h_pcoff.resize(pipe_paths ? nseq : 0);
+    h_fcoff.resize(pipe_paths ? nseq : 0);
+    uint64_t bytes = 0, bpn = 0, cmn = 0, hrn = 0, ckn = 0, pmn = 0, prn = 0, pcn = 0, fcn = 0;
     for (uint32_t q = 0; q < nseq; ++q) {
         if (offs[q + 1] < offs[q]) throw Error(SVH_E_INVALID, "offsets must be non-decreasing");
         const uint64_t len = offs[q + 1] - offs[q];
@@ -1186,6 +1226,16 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
             hrn += chain_hrec_words(len);
             h_ckoff[q] = ckn;
             ckn += chain_ckpt_floats(len, cpl->plan.SM, cpl->plan.B);
+            if (ppl) {
+                h_pmoff[q] = pmn;
+                pmn += pipe_mask_words(len, ppl->plan.nblk, ppl->plan.SM);
+                h_proff[q] = prn;
+                prn += pipe_prec_count(len, ppl->plan.nblk);
+                h_pcoff[q] = pcn;
+                pcn += pipe_ckpt_floats(len, ppl->plan.P);
+                h_fcoff[q] = fcn;
+                fcn += pipe_fck_floats(len);
+            }
         } else if (paths) {
             h_bpoff[q] = bpn;
             bpn += (len - 1) * (uint64_t)model->host.n;
@@ -1220,6 +1270,16 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
         d_hrecoff.upload_async(h_hroff.data(), (size_t)nseq * 8, s);
         d_ckpt.reserve((size_t)std::max<uint64_t>(ckn, 1) * 4);
         d_ckptoff.upload_async(h_ckoff.data(), (size_t)nseq * 8, s);
+        if (pipe_paths) {
+            d_pmask.reserve((size_t)std::max<uint64_t>(pmn, 1) * 4);
+            d_pmaskoff.upload_async(h_pmoff.data(), (size_t)nseq * 8, s);
+            d_prec.reserve((size_t)std::max<uint64_t>(prn, 1) * 8);
+            d_precoff.upload_async(h_proff.data(), (size_t)nseq * 8, s);
+            d_pck.reserve((size_t)std::max<uint64_t>(pcn, 1) * 4);
+            d_pckoff.upload_async(h_pcoff.data(), (size_t)nseq * 8, s);
+            d_fck.reserve((size_t)std::max<uint64_t>(fcn, 1) * 4);
+            d_fckoff.upload_async(h_fcoff.data(), (size_t)nseq * 8, s);
+        }
     } else if (paths) {
         d_bp.reserve((size_t)std::max<uint64_t>(bpn, 1) * 2);
         d_bpoff.upload_async(h_bpoff.data(), (size_t)nseq * 8, s);
@@ -1280,7 +1340,36 @@ void Batch::run(uint32_t level, hipStream_t s) {
     auto launch_step_kernel = [&](const FusedBatch& b, bool want_paths) { model->launch_steps(b, want_paths, s); };
 
     hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
-    if (level <= 1) {
+    if (level <= 1 && pipe_paths) {
+        // decoded paths on the pipelined plan: its path variant, the chain path variant for rows
+        // whose speculation failed, the pipelined traceback (unflagged rows), the chain traceback
+        // (flagged rows)
+        const DevicePipePlan* ppl = model->pipe_paths_for(nseq);
+        const DeviceBandPlan* bpl = model->band_for(true);
+        if (!ppl || !bpl) throw Error(SVH_E_STATE, "batch planned for pipelined paths, model has no such plan");
+        pipe.ensure(nseq, ppl->plan.G, s);
+        pipe.note_launch(s);
+        FusedBatch pb = fb;
+        pb.cmask = d_pmask.as<uint32_t>();
+        pb.cmask_off = d_pmaskoff.as<uint64_t>();
+        pb.ckpt = d_pck.as<float>();
+        pb.ckpt_off = d_pckoff.as<uint64_t>();
+        pb.prec = d_prec.as<float2>();
+        pb.prec_off = d_precoff.as<uint64_t>();
+        pb.fck = d_fck.as<float>();
+        pb.fck_off = d_fckoff.as<uint64_t>();
+        pb.pipe = &pipe.view;
+        hip_check(launch_pipe(ppl->view, pb, pipe.view, s), "pipelined Viterbi kernel (paths)");
+        FusedBatch cb = fb;  // chain buffers
+        cb.run_mask = pipe.view.viol;
+        hip_check(launch_chain(bpl->view, 1, cb, s), "chain Viterbi kernel (pipe paths fallback)");
+        hip_check(launch_pipe_traceback(ppl->view, pb, d_pathoff.as<uint64_t>(), d_paths.as<int32_t>(),
+                                        pipe.view.viol, s),
+                  "pipelined traceback kernel");
+        hip_check(launch_chain_traceback(bpl->view, cb, d_pathoff.as<uint64_t>(), d_paths.as<int32_t>(), s),
+                  "chain traceback kernel (pipe paths fallback)");
+        pipe_ran = true;
+    } else if (level <= 1) {
         launch_step_kernel(fb, paths);
         if (paths && chain_paths)
             hip_check(launch_chain_traceback(model->band_for(true)->view, fb, d_pathoff.as<uint64_t>(),

@@ -139,13 +139,18 @@ struct PipePlan {
     std::vector<uint32_t> lrow; // [P]
     std::vector<float> hc;      // [S][8]
     bool wide = false;          // pipe_wide.hip layout: tab [nblk][S][SM/2][64][4], W sequences per workgroup
+    // decoded paths (PipeModel::pflags / spos / hx_exist / hl_exist / ties_heavy)
+    std::vector<uint8_t> pflags;  // [P]
+    std::vector<int32_t> spos;    // [n]
+    uint32_t hx_exist = 0, hl_exist = 0;
+    bool ties_heavy = false;
 };
 // sm = 0 / waves = 0: defaults (SVH_PIPE_SM / SVH_PIPE_WAVES override them, diagnostics)
 PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm = 0, uint32_t waves = 0, bool wide = false);
 
 struct DevicePipePlan {
     PipePlan plan;
-    DeviceBuffer d_tab, d_e0, d_start, d_lrow, d_hc, d_stamps;
+    DeviceBuffer d_tab, d_e0, d_start, d_lrow, d_hc, d_stamps, d_pflags, d_spos;
     PipeModel view{};
     void upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream_t s);
     void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_PIPE_DEBUG): first sequence's waves
@@ -220,6 +225,9 @@ struct Model {
     const DeviceBandPlan* band_for(bool paths, uint32_t nseq = 0) const;
     // Pipelined plan for a scores-only pass over nseq rows (nullptr: none).
     const DevicePipePlan* pipe_for(uint32_t nseq) const;
+    // Pipelined plan for a decoded-path pass over nseq rows (nullptr: the chain / fused variant):
+    // the latency plan, with the chain kernel's path variant as the fallback of flagged rows.
+    const DevicePipePlan* pipe_paths_for(uint32_t nseq) const;
     void spec_build(uint32_t level, hipStream_t s);
     svh_model_info info(uint32_t nseq = 0, bool paths = false, uint32_t level = 0) const;
     // one pass of the step kernel the model plans for (chain, band, fused or generic)
@@ -237,6 +245,10 @@ struct Batch {
     DeviceBuffer d_bp, d_bpoff, d_pathoff, d_paths;
     bool chain_paths = false;  // paths from the chain kernel's compact records (else fused / generic)
     DeviceBuffer d_cmask, d_cmaskoff, d_hrec, d_hrecoff, d_ckpt, d_ckptoff;
+    // paths on the pipelined plan (pipe.hip PATHS): its masks, partial records, checkpoints and F
+    // checkpoints (the heavy records share d_hrec: the chain fallback writes only flagged rows)
+    bool pipe_paths = false;
+    DeviceBuffer d_pmask, d_pmaskoff, d_prec, d_precoff, d_pck, d_pckoff, d_fck, d_fckoff;
     PipeScratchBuffers pipe;  // pipelined kernel scratch (sized for the rows of each launch)
     // fault word of this batch's runs (FusedBatch::fault; kFault* bits): only this batch's
     // kernels write it and only this batch reads and clears it
@@ -252,6 +264,7 @@ struct Batch {
     std::vector<uint8_t> h_sym;
     Pinned<uint8_t> h_out;  // read(): scores, best and the fault words land here in one sync
     std::vector<uint64_t> h_symoff, h_pathoff, h_bpoff, h_cmoff, h_hroff, h_ckoff;
+    std::vector<uint64_t> h_pmoff, h_proff, h_pcoff, h_fcoff;
     std::vector<uint32_t> h_zero;
 
     Batch(Model* m, uint64_t nseq, const uint64_t* offsets, const uint64_t* symbols, uint32_t flags);

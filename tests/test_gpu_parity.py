@@ -252,17 +252,24 @@ def test_chain_decoded_paths(L, kw, seed):
     entry identical to the oracle's lexicographic (value, row) argmin, over lengths 1..5000."""
     hmm = random_chain_hmm(L, seed=seed, **kw)
     seqs = random_seqs(20, [1, 2, 3, 4, 5, 6, 7, 8, 9, 63, 64, 65, 77, 1000, 5000], seed=seed)
+    # AUTO: the pipelined plan's path variant where the model has one (chain fallback), else the
+    # chain or fused variant; then the chain variant forced
     model = check_against_oracle(hmm, seqs, paths=True)
-    want = _lib.SVH_KERNEL_FUSED if kw.get("feed_c") else _lib.SVH_KERNEL_CHAIN
+    info = model.info()
+    want = (_lib.SVH_KERNEL_FUSED if kw.get("feed_c") else
+            _lib.SVH_KERNEL_PIPE if info["pipe_slots"] > 0 else _lib.SVH_KERNEL_CHAIN)
     if L >= 2:
-        assert model.info()["paths_kernel"] == want, model.info()
+        assert info["paths_kernel"] == want, info
+    if L >= 2 and not kw.get("feed_c"):
+        model = check_against_oracle(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN, paths=True)
+        assert model.info()["paths_kernel"] == _lib.SVH_KERNEL_CHAIN, model.info()
 
 
 def test_chain_paths_covid_2405():
     """covid-19.ess (38..7096 observations, symbol refills) on 2405.chmm: chain decoded paths."""
     hmm = svh.read_HMM(chmm("2405.chmm"))
     seqs = svh.read_emit_seq(ess("covid-19.ess"))
-    model = check_against_oracle(hmm, seqs, paths=True)
+    model = check_against_oracle(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN, paths=True)
     assert model.info()["paths_kernel"] == _lib.SVH_KERNEL_CHAIN
 
 
@@ -270,7 +277,7 @@ def test_chain_paths_covid_2405():
 def test_chain_paths_geometries(threads):
     hmm = svh.read_HMM(chmm("300.chmm"))
     seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
-    model = check_against_oracle(hmm, seqs, max_threads=threads, paths=True)
+    model = check_against_oracle(hmm, seqs, kernel=_lib.SVH_KERNEL_CHAIN, max_threads=threads, paths=True)
     assert model.info()["paths_kernel"] == _lib.SVH_KERNEL_CHAIN
 
 
@@ -281,7 +288,10 @@ def test_chain_paths_match_fused_paths():
         if not name.endswith(".chmm"):
             continue
         hmm = svh.read_HMM(chmm(name))
-        a = svh.DeviceModel(hmm)
+        try:
+            a = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_CHAIN)
+        except _lib.SvhError:  # not chain-shaped
+            continue
         if a.info()["paths_kernel"] != _lib.SVH_KERNEL_CHAIN:
             continue
         b = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_FUSED)
