@@ -12,7 +12,8 @@ LIB      := spec_viterbi_amd/libspec_viterbi_hip.so
 ORACLE   := oracle/liboracle.so
 
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) \
-            -fno-honor-nans -mllvm -amdgpu-atomic-optimizer-strategy=None -Wall -Wno-unused-parameter
+            -fno-honor-nans -mllvm -amdgpu-atomic-optimizer-strategy=None -Wall -Wno-unused-parameter \
+            $(EXTRA_HIPFLAGS)
 HOSTFLAGS := --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall
 
 HIP_SRCS  := $(wildcard $(CSRC)/fused_*.hip) $(CSRC)/misc.hip $(CSRC)/band.hip $(wildcard $(CSRC)/chain_*.hip) $(CSRC)/timepar.hip $(CSRC)/pipe.hip \

@@ -1181,8 +1181,6 @@ void Batch::init(uint32_t flags) {
     DeviceGuard g(model->device);
     hip_check(hipEventCreate(&ev_start), "hipEventCreate");
     hip_check(hipEventCreate(&ev_stop), "hipEventCreate");
-    d_fault.alloc(sizeof(uint32_t));
-    hip_check(hipMemsetAsync(d_fault.ptr, 0, sizeof(uint32_t), model->stream), "fault word");
 }
 
 // (Re)load the batch's sequences: host packing, then asynchronous uploads on `s` into device
@@ -1243,51 +1241,119 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
         h_pathoff[q] = offs[q] - offs[0];
     }
     total = offs[nseq] - offs[0];
-    h_sym.assign(bytes, 0);
+    DeviceGuard g(model->device);
+    // Every input table of the batch -- symbols, then the per-sequence offset / begin / end
+    // tables -- in one pinned staging arena and one asynchronous upload into one device arena
+    // (separate pageable copies each cost a staging round trip; the symbols are converted from
+    // the caller's uint64 straight into pinned memory).  The staging arena is reused by the next
+    // load, which always follows the completion of this batch's previous run.
+    struct Section {
+        size_t off = 0, bytes = 0;
+    };
+    size_t in_bytes = 0;
+    auto section = [&](size_t nb) {
+        Section x;
+        x.off = in_bytes;
+        x.bytes = nb;
+        in_bytes += (nb + 15) & ~(size_t)15;
+        return x;
+    };
+    const Section s_sym = section(bytes), s_symoff = section((size_t)nseq * 8), s_begin = section((size_t)nseq * 4),
+                  s_end = section((size_t)nseq * 4);
+    const bool cp = paths && chain_paths, pp = cp && pipe_paths, fp = paths && !chain_paths;
+    const Section s_path = section(paths ? (size_t)nseq * 8 : 0), s_cm = section(cp ? (size_t)nseq * 8 : 0),
+                  s_hr = section(cp ? (size_t)nseq * 8 : 0), s_ck = section(cp ? (size_t)nseq * 8 : 0),
+                  s_pm = section(pp ? (size_t)nseq * 8 : 0), s_pr = section(pp ? (size_t)nseq * 8 : 0),
+                  s_pc = section(pp ? (size_t)nseq * 8 : 0), s_fc = section(pp ? (size_t)nseq * 8 : 0),
+                  s_bp = section(fp ? (size_t)nseq * 8 : 0);
+    uint8_t* const hin = h_in.reserve(in_bytes);
     const uint64_t S = model->host.S;
     for (uint32_t q = 0; q < nseq; ++q) {
-        uint8_t* dstp = h_sym.data() + h_symoff[q];
-        for (uint32_t i = 0; i < lens[q]; ++i) {
-            const uint64_t x = sym64 ? sym64[offs[q] + i] : sym8[offs[q] + i];
-            if (x >= S)
-                throw Error(SVH_E_RANGE, "symbol " + std::to_string(x) + " out of range (emit_num " +
-                                             std::to_string(S) + ")");
-            dstp[i] = (uint8_t)x;
+        uint8_t* dstp = hin + s_sym.off + h_symoff[q];
+        const uint32_t L = lens[q];
+        const uint64_t base = offs[q];
+        if (sym64) {
+            uint64_t bad = 0;
+            for (uint32_t i = 0; i < L; ++i) {
+                const uint64_t x = sym64[base + i];
+                bad |= x >= S ? 1u : 0u;
+                dstp[i] = (uint8_t)x;
+            }
+            if (bad)
+                for (uint32_t i = 0; i < L; ++i)
+                    if (sym64[base + i] >= S)
+                        throw Error(SVH_E_RANGE, "symbol " + std::to_string(sym64[base + i]) +
+                                                     " out of range (emit_num " + std::to_string(S) + ")");
+        } else {
+            for (uint32_t i = 0; i < L; ++i) {
+                const uint64_t x = sym8[base + i];
+                if (x >= S)
+                    throw Error(SVH_E_RANGE, "symbol " + std::to_string(x) + " out of range (emit_num " +
+                                                 std::to_string(S) + ")");
+                dstp[i] = (uint8_t)x;
+            }
         }
+        // zero padding after the sequence (kSymPad and the 16-byte round-up)
+        const uint64_t end = q + 1 < nseq ? h_symoff[q + 1] : bytes;
+        std::memset(dstp + L, 0, end - h_symoff[q] - L);
     }
-    h_zero.assign(nseq, 0);
-    DeviceGuard g(model->device);
-    d_sym.upload_async(h_sym.data(), h_sym.size(), s);
-    d_symoff.upload_async(h_symoff.data(), (size_t)nseq * 8, s);
-    d_begin.upload_async(h_zero.data(), (size_t)nseq * 4, s);
-    d_end.upload_async(lens.data(), (size_t)nseq * 4, s);
-    d_scores.reserve((size_t)nseq * model->host.n * 4);
-    d_best.reserve((size_t)nseq * 8);
-    if (paths && chain_paths) {
+    auto put = [&](const Section& x, const void* src) {
+        if (x.bytes) std::memcpy(hin + x.off, src, x.bytes);
+    };
+    put(s_symoff, h_symoff.data());
+    std::memset(hin + s_begin.off, 0, s_begin.bytes);
+    put(s_end, lens.data());
+    put(s_path, h_pathoff.data());
+    put(s_cm, h_cmoff.data());
+    put(s_hr, h_hroff.data());
+    put(s_ck, h_ckoff.data());
+    put(s_pm, h_pmoff.data());
+    put(s_pr, h_proff.data());
+    put(s_pc, h_pcoff.data());
+    put(s_fc, h_fcoff.data());
+    put(s_bp, h_bpoff.data());
+    d_in.reserve(in_bytes);
+    hip_check(hipMemcpyAsync(d_in.ptr, hin, in_bytes, hipMemcpyHostToDevice, s), "batch inputs H2D");
+    uint8_t* const din = d_in.as<uint8_t>();
+    p_sym = din + s_sym.off;
+    p_symoff = reinterpret_cast<uint64_t*>(din + s_symoff.off);
+    p_begin = reinterpret_cast<uint32_t*>(din + s_begin.off);
+    p_end = reinterpret_cast<uint32_t*>(din + s_end.off);
+    auto u64p = [&](const Section& x) { return x.bytes ? reinterpret_cast<uint64_t*>(din + x.off) : nullptr; };
+    p_pathoff = u64p(s_path);
+    p_cmoff = u64p(s_cm);
+    p_hroff = u64p(s_hr);
+    p_ckoff = u64p(s_ck);
+    p_pmoff = u64p(s_pm);
+    p_proff = u64p(s_pr);
+    p_pcoff = u64p(s_pc);
+    p_fcoff = u64p(s_fc);
+    p_bpoff = u64p(s_bp);
+    // results: fault word | best states | scores, one device arena (read() copies it at once); a
+    // grown arena starts with a clear fault word
+    const size_t best_off = 16, score_off = best_off + (((size_t)nseq * 8 + 15) & ~(size_t)15);
+    const size_t out_bytes = score_off + (size_t)nseq * model->host.n * 4;
+    if (!d_out.ptr || out_bytes > d_out.bytes) {
+        d_out.alloc(out_bytes);
+        hip_check(hipMemsetAsync(d_out.ptr, 0, 16, s), "fault word");
+    }
+    p_fault = d_out.as<uint32_t>();
+    p_best = reinterpret_cast<int64_t*>(d_out.as<uint8_t>() + best_off);
+    p_scores = reinterpret_cast<float*>(d_out.as<uint8_t>() + score_off);
+    if (cp) {
         d_cmask.reserve((size_t)std::max<uint64_t>(cmn, 1) * 4);
-        d_cmaskoff.upload_async(h_cmoff.data(), (size_t)nseq * 8, s);
         d_hrec.reserve((size_t)std::max<uint64_t>(hrn, kRecWords) * 4);
-        d_hrecoff.upload_async(h_hroff.data(), (size_t)nseq * 8, s);
         d_ckpt.reserve((size_t)std::max<uint64_t>(ckn, 1) * 4);
-        d_ckptoff.upload_async(h_ckoff.data(), (size_t)nseq * 8, s);
-        if (pipe_paths) {
+        if (pp) {
             d_pmask.reserve((size_t)std::max<uint64_t>(pmn, 1) * 4);
-            d_pmaskoff.upload_async(h_pmoff.data(), (size_t)nseq * 8, s);
             d_prec.reserve((size_t)std::max<uint64_t>(prn, 1) * 8);
-            d_precoff.upload_async(h_proff.data(), (size_t)nseq * 8, s);
             d_pck.reserve((size_t)std::max<uint64_t>(pcn, 1) * 4);
-            d_pckoff.upload_async(h_pcoff.data(), (size_t)nseq * 8, s);
             d_fck.reserve((size_t)std::max<uint64_t>(fcn, 1) * 4);
-            d_fckoff.upload_async(h_fcoff.data(), (size_t)nseq * 8, s);
         }
-    } else if (paths) {
+    } else if (fp) {
         d_bp.reserve((size_t)std::max<uint64_t>(bpn, 1) * 2);
-        d_bpoff.upload_async(h_bpoff.data(), (size_t)nseq * 8, s);
     }
-    if (paths) {
-        d_pathoff.upload_async(h_pathoff.data(), (size_t)nseq * 8, s);
-        d_paths.reserve((size_t)std::max<uint64_t>(total, 1) * 4);
-    }
+    if (paths) d_paths.reserve((size_t)std::max<uint64_t>(total, 1) * 4);
     spec_ready_level = 0;
     ran = false;
     pipe_ran = false;
@@ -1311,24 +1377,24 @@ void Batch::run(uint32_t level, hipStream_t s) {
     const CsrModel csr = model->csr_view();
     FusedBatch fb;
     std::memset(&fb, 0, sizeof(fb));
-    fb.symbols = d_sym.as<uint8_t>();
-    fb.sym_off = d_symoff.as<uint64_t>();
-    fb.begin = d_begin.as<uint32_t>();
-    fb.end = d_end.as<uint32_t>();
-    fb.scores = d_scores.as<float>();
-    fb.best = d_best.as<int64_t>();
-    fb.fault = d_fault.as<uint32_t>();
+    fb.symbols = p_sym;
+    fb.sym_off = p_symoff;
+    fb.begin = p_begin;
+    fb.end = p_end;
+    fb.scores = p_scores;
+    fb.best = p_best;
+    fb.fault = p_fault;
     fb.nseq = nseq;
     if (paths && chain_paths) {
         fb.cmask = d_cmask.as<uint32_t>();
-        fb.cmask_off = d_cmaskoff.as<uint64_t>();
+        fb.cmask_off = p_cmoff;
         fb.hrec = d_hrec.as<uint32_t>();
-        fb.hrec_off = d_hrecoff.as<uint64_t>();
+        fb.hrec_off = p_hroff;
         fb.ckpt = d_ckpt.as<float>();
-        fb.ckpt_off = d_ckptoff.as<uint64_t>();
+        fb.ckpt_off = p_ckoff;
     } else if (paths) {
         fb.bp = d_bp.as<uint16_t>();
-        fb.bp_off = d_bpoff.as<uint64_t>();
+        fb.bp_off = p_bpoff;
     }
     pipe_ran = false;
     if (const DevicePipePlan* pp = paths ? nullptr : model->pipe_for(nseq)) {  // pipelined plan: scratch
@@ -1351,32 +1417,32 @@ void Batch::run(uint32_t level, hipStream_t s) {
         pipe.note_launch(s);
         FusedBatch pb = fb;
         pb.cmask = d_pmask.as<uint32_t>();
-        pb.cmask_off = d_pmaskoff.as<uint64_t>();
+        pb.cmask_off = p_pmoff;
         pb.ckpt = d_pck.as<float>();
-        pb.ckpt_off = d_pckoff.as<uint64_t>();
+        pb.ckpt_off = p_pcoff;
         pb.prec = d_prec.as<float2>();
-        pb.prec_off = d_precoff.as<uint64_t>();
+        pb.prec_off = p_proff;
         pb.fck = d_fck.as<float>();
-        pb.fck_off = d_fckoff.as<uint64_t>();
+        pb.fck_off = p_fcoff;
         pb.pipe = &pipe.view;
         hip_check(launch_pipe(ppl->view, pb, pipe.view, s), "pipelined Viterbi kernel (paths)");
         FusedBatch cb = fb;  // chain buffers
         cb.run_mask = pipe.view.viol;
         hip_check(launch_chain(bpl->view, 1, cb, s), "chain Viterbi kernel (pipe paths fallback)");
-        hip_check(launch_pipe_traceback(ppl->view, pb, d_pathoff.as<uint64_t>(), d_paths.as<int32_t>(),
+        hip_check(launch_pipe_traceback(ppl->view, pb, p_pathoff, d_paths.as<int32_t>(),
                                         pipe.view.viol, s),
                   "pipelined traceback kernel");
-        hip_check(launch_chain_traceback(bpl->view, cb, d_pathoff.as<uint64_t>(), d_paths.as<int32_t>(), s),
+        hip_check(launch_chain_traceback(bpl->view, cb, p_pathoff, d_paths.as<int32_t>(), s),
                   "chain traceback kernel (pipe paths fallback)");
         pipe_ran = true;
     } else if (level <= 1) {
         launch_step_kernel(fb, paths);
         if (paths && chain_paths)
-            hip_check(launch_chain_traceback(model->band_for(true)->view, fb, d_pathoff.as<uint64_t>(),
+            hip_check(launch_chain_traceback(model->band_for(true)->view, fb, p_pathoff,
                                              d_paths.as<int32_t>(), s),
                       "chain traceback kernel");
         else if (paths)
-            hip_check(launch_traceback(fb, d_pathoff.as<uint64_t>(), d_paths.as<int32_t>(), model->host.n, s),
+            hip_check(launch_traceback(fb, p_pathoff, d_paths.as<int32_t>(), model->host.n, s),
                       "traceback kernel");
     } else {
         const uint32_t n = model->host.n;
@@ -1526,9 +1592,9 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
         const size_t orow = table32(vrow);
         vbeg.clear();
         vend.clear();
-        const uint8_t* sym = d_sym.as<uint8_t>();
+        const uint8_t* sym = p_sym;
         int64_t* vbest = d_vbest.as<int64_t>();
-        uint32_t* fault = d_fault.as<uint32_t>();
+        uint32_t* fault = p_fault;
         Model* mdl = model;
         ops.push_back([=](const uint8_t* base) {
             FusedBatch fb;
@@ -1654,8 +1720,8 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
         nflags += na;
     }
     {
-        int64_t* const best_ = d_best.as<int64_t>();
-        float* const scores_ = d_scores.as<float>();
+        int64_t* const best_ = p_best;
+        float* const scores_ = p_scores;
         const uint32_t ns = nseq;
         ops.push_back([=](const uint8_t*) {
             hip_check(launch_tp_finish(S_, scores_, best_, ns, n, s), "time-parallel finish");
@@ -1683,24 +1749,26 @@ void Batch::read(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out
     if (!s) s = model->stream;
     if (!ran) throw Error(SVH_E_STATE, "svh_batch_read before svh_batch_run");
     if (paths_out && !paths) throw Error(SVH_E_STATE, "batch was created without SVH_BATCH_PATHS");
-    // scores, best states and the batch's fault word into pinned staging on the run's stream,
-    // one synchronisation, then out to the caller (pageable copies would each block on their own)
+    // the fault word, best states and scores (one device arena: one copy) and the paths into
+    // pinned staging on the run's stream, one synchronisation, then out to the caller (pageable
+    // copies would each block on their own)
     const size_t sb = scores ? (size_t)nseq * model->host.n * 4 : 0, bb = best ? (size_t)nseq * 8 : 0;
-    constexpr size_t fb = 16;  // the fault word, padded (keeps the scores 16-byte aligned)
-    uint8_t* st = h_out.reserve(fb + sb + bb);
-    hip_check(hipMemcpyAsync(st, d_fault.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "fault D2H");
-    if (sb) hip_check(hipMemcpyAsync(st + fb, d_scores.ptr, sb, hipMemcpyDeviceToHost, s), "scores D2H");
-    if (bb) hip_check(hipMemcpyAsync(st + fb + sb, d_best.ptr, bb, hipMemcpyDeviceToHost, s), "best D2H");
+    const size_t best_off = (size_t)(reinterpret_cast<uint8_t*>(p_best) - d_out.as<uint8_t>());
+    const size_t score_off = (size_t)(reinterpret_cast<uint8_t*>(p_scores) - d_out.as<uint8_t>());
+    const size_t pre = sb ? score_off + sb : bb ? best_off + bb : 16;
+    const size_t pb = paths_out ? (size_t)total * 4 : 0, path_off = (pre + 15) & ~(size_t)15;
+    uint8_t* st = h_out.reserve(path_off + pb);
+    hip_check(hipMemcpyAsync(st, d_out.ptr, pre, hipMemcpyDeviceToHost, s), "results D2H");
+    if (pb) hip_check(hipMemcpyAsync(st + path_off, d_paths.ptr, pb, hipMemcpyDeviceToHost, s), "paths D2H");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     {
         uint32_t f;
         std::memcpy(&f, st, sizeof(f));
         report_fault(f, s);
     }
-    if (sb) std::memcpy(scores, st + fb, sb);
-    if (bb) std::memcpy(best, st + fb + sb, bb);
-    if (paths_out)
-        hip_check(hipMemcpy(paths_out, d_paths.ptr, (size_t)total * 4, hipMemcpyDeviceToHost), "paths D2H");
+    if (sb) std::memcpy(scores, st + score_off, sb);
+    if (bb) std::memcpy(best, st + best_off, bb);
+    if (pb) std::memcpy(paths_out, st + path_off, pb);
 }
 
 void Batch::read_async(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out) {
@@ -1708,9 +1776,9 @@ void Batch::read_async(hipStream_t s, float* scores, int64_t* best, int32_t* pat
     if (!ran) throw Error(SVH_E_STATE, "read before run");
     if (paths_out && !paths) throw Error(SVH_E_STATE, "batch was created without SVH_BATCH_PATHS");
     if (scores)
-        hip_check(hipMemcpyAsync(scores, d_scores.ptr, (size_t)nseq * model->host.n * 4, hipMemcpyDeviceToHost, s),
+        hip_check(hipMemcpyAsync(scores, p_scores, (size_t)nseq * model->host.n * 4, hipMemcpyDeviceToHost, s),
                   "scores D2H");
-    if (best) hip_check(hipMemcpyAsync(best, d_best.ptr, (size_t)nseq * 8, hipMemcpyDeviceToHost, s), "best D2H");
+    if (best) hip_check(hipMemcpyAsync(best, p_best, (size_t)nseq * 8, hipMemcpyDeviceToHost, s), "best D2H");
     if (paths_out)
         hip_check(hipMemcpyAsync(paths_out, d_paths.ptr, (size_t)total * 4, hipMemcpyDeviceToHost, s), "paths D2H");
 }
@@ -1756,7 +1824,7 @@ void Batch::check_fault(hipStream_t s) {
     DeviceGuard g(model->device);
     if (!s) s = model->stream;
     uint32_t* f = reinterpret_cast<uint32_t*>(h_out.reserve(16));
-    hip_check(hipMemcpyAsync(f, d_fault.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "fault D2H");
+    hip_check(hipMemcpyAsync(f, p_fault, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "fault D2H");
     hip_check(hipStreamSynchronize(s), "fault D2H");
     report_fault(*f, s);
 }
@@ -1765,7 +1833,7 @@ void Batch::report_fault(uint32_t f, hipStream_t s) {
     if (!f) return;
     // reported once: clear the word (ordered on the stream of the run that set it) so this batch's
     // later runs are judged on their own; other batches have words of their own
-    hip_check(hipMemsetAsync(d_fault.ptr, 0, sizeof(uint32_t), s), "fault reset");
+    hip_check(hipMemsetAsync(p_fault, 0, sizeof(uint32_t), s), "fault reset");
     if (f & (kFaultPipe | kFaultPipeWide))
         throw Error(SVH_E_HIP, "pipelined kernel: a bounded wait gave up (results invalid)");
     throw Error(SVH_E_HIP, "chain kernel: a bounded inter-wave wait gave up (results invalid)");
@@ -1775,7 +1843,7 @@ void Batch::inject_fault(hipStream_t s) {
     DeviceGuard g(model->device);
     if (!s) s = model->stream;
     if (!ran) throw Error(SVH_E_STATE, "no run recorded");
-    hip_check(hipMemsetAsync(d_fault.ptr, 0x01, 1, s), "fault inject");  // kFaultPipe
+    hip_check(hipMemsetAsync(p_fault, 0x01, 1, s), "fault inject");  // kFaultPipe
 }
 
 uint64_t Batch::pipe_fallbacks() {

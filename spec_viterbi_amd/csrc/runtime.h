@@ -241,18 +241,31 @@ struct Batch {
     std::vector<uint64_t> offsets;  // host copy of the caller's prefix offsets
     std::vector<uint32_t> lens;
     uint64_t total = 0;
-    DeviceBuffer d_sym, d_symoff, d_begin, d_end, d_scores, d_best;
-    DeviceBuffer d_bp, d_bpoff, d_pathoff, d_paths;
+    // inputs: one device arena (symbols, offset / begin / end tables, path offset tables),
+    // uploaded from one pinned staging arena per load; the pointers are views into it
+    DeviceBuffer d_in;
+    Pinned<uint8_t> h_in;
+    uint8_t* p_sym = nullptr;
+    uint64_t* p_symoff = nullptr;
+    uint32_t *p_begin = nullptr, *p_end = nullptr;
+    uint64_t *p_pathoff = nullptr, *p_cmoff = nullptr, *p_hroff = nullptr, *p_ckoff = nullptr, *p_pmoff = nullptr,
+             *p_proff = nullptr, *p_pcoff = nullptr, *p_fcoff = nullptr, *p_bpoff = nullptr;
+    // results: one device arena {fault word (16 B) | best states | scores}: read() copies it once.
+    // The fault word (FusedBatch::fault; kFault* bits) is written only by this batch's kernels
+    // and read and cleared only by this batch.
+    DeviceBuffer d_out;
+    uint32_t* p_fault = nullptr;
+    int64_t* p_best = nullptr;
+    float* p_scores = nullptr;
+    DeviceBuffer d_bp, d_paths;
     bool chain_paths = false;  // paths from the chain kernel's compact records (else fused / generic)
-    DeviceBuffer d_cmask, d_cmaskoff, d_hrec, d_hrecoff, d_ckpt, d_ckptoff;
+    DeviceBuffer d_cmask, d_hrec, d_ckpt;
     // paths on the pipelined plan (pipe.hip PATHS): its masks, partial records, checkpoints and F
     // checkpoints (the heavy records share d_hrec: the chain fallback writes only flagged rows)
     bool pipe_paths = false;
-    DeviceBuffer d_pmask, d_pmaskoff, d_prec, d_precoff, d_pck, d_pckoff, d_fck, d_fckoff;
+    DeviceBuffer d_pmask, d_prec, d_pck, d_fck;
     PipeScratchBuffers pipe;  // pipelined kernel scratch (sized for the rows of each launch)
-    // fault word of this batch's runs (FusedBatch::fault; kFault* bits): only this batch's
-    // kernels write it and only this batch reads and clears it
-    DeviceBuffer d_fault;
+
     // _spec runs
     DeviceBuffer d_vbuf, d_nchunks, d_tbegin, d_vrow;
     uint32_t spec_ready_level = 0;
@@ -260,12 +273,10 @@ struct Batch {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     bool ran = false;
 
-    // host staging of the last load (kept alive for the asynchronous uploads)
-    std::vector<uint8_t> h_sym;
-    Pinned<uint8_t> h_out;  // read(): scores, best and the fault words land here in one sync
+    // host tables of the last load (copied into h_in)
+    Pinned<uint8_t> h_out;  // read(): the result arena and the paths land here in one sync
     std::vector<uint64_t> h_symoff, h_pathoff, h_bpoff, h_cmoff, h_hroff, h_ckoff;
     std::vector<uint64_t> h_pmoff, h_proff, h_pcoff, h_fcoff;
-    std::vector<uint32_t> h_zero;
 
     Batch(Model* m, uint64_t nseq, const uint64_t* offsets, const uint64_t* symbols, uint32_t flags);
     Batch(Model* m, uint64_t nseq, const uint64_t* offsets, const uint8_t* symbols, uint32_t flags);

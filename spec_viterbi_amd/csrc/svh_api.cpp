@@ -250,8 +250,8 @@ int svh_batch_read(svh_batch_t b, void* stream, float* scores, int64_t* best_sta
 int svh_batch_device_results(svh_batch_t b, float** scores, int64_t** best_state) {
     return guarded([&] {
         require(b != nullptr, "null batch");
-        if (scores) *scores = b->impl->d_scores.as<float>();
-        if (best_state) *best_state = b->impl->d_best.as<int64_t>();
+        if (scores) *scores = b->impl->p_scores;
+        if (best_state) *best_state = b->impl->p_best;
     });
 }
 

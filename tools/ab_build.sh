@@ -1,0 +1,11 @@
+#!/bin/bash
+# Build a variant of the engine library for A/B timing on the GPU box:
+#   tools/ab_build.sh NAME "EXTRA HIPFLAGS"   -> build_ab/NAME/libspec_viterbi_hip.so
+# (sources from the tree, e.g. -DSVH_PIPE_HK=0).  Run with SVH_LIB=build_ab/NAME/libspec_viterbi_hip.so.
+set -e
+cd "$(dirname "$0")/.."
+NAME=$1; FLAGS=$2
+D=build_ab/$NAME
+mkdir -p $D
+make -j8 BUILD=$D/obj LIB=$D/libspec_viterbi_hip.so EXTRA_HIPFLAGS="$FLAGS" $D/libspec_viterbi_hip.so > $D/build.log 2>&1
+echo "built $D/libspec_viterbi_hip.so"
