@@ -133,7 +133,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 
     float v[SM];  // light scores of the lane's positions
     f2 CF;        // {S partial of this lane, F'} (one register pair: the packed heavy update)
-    uint64_t viol = 0;
+    uint32_t viol = 0;  // per lane: steps whose check failed (a VGPR count: no VALU -> SALU hand-off)
     uint32_t spins = 0;
     // PATHS: the last 32 "took F's term" bits per slot (bit 0 = newest), the static tie masks
     // (PATHS 1), the lane's light minimum of the last step's input scores
@@ -320,13 +320,12 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             const f2 s2 = (f2){kxss, kxff} + CF;          // X_SS + c, X_FF + F
             float cn = fminf(s1.x, s2.x);
             if constexpr (SX) cn = fminf(cn, readlane_f(cXSF, o) + CF.y);
-            {  // viol |= [A_F + m < F'] per lane, folded at once (not held per step by the compiler)
-                uint64_t c;
-                asm volatile("v_cmp_lt_f32_e64 %1, %2, %3\n\ts_or_b64 %0, %0, %1"
-                             : "+s"(viol), "=&s"(c)
-                             : "v"(s1.y), "v"(s2.y)
-                             : "scc");
-            }
+            // viol += [A_F + m < F'] per lane: compare into VCC, add with carry-in (two VALU, no
+            // VALU -> SALU dependency per step)
+            asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+                         : "+v"(viol)
+                         : "v"(s1.y), "v"(s2.y)
+                         : "vcc");
             CF = (f2){cn, s2.y};
 #pragma unroll
             for (int s = 0; s < SM; ++s) v[s] = vn[s];
@@ -630,11 +629,12 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         }
         wave_lexmin63(bvv, bk);
         const float cmin = wave_min63(CF.x);
+        const bool any_viol = __builtin_amdgcn_ballot_w64(viol != 0) != 0;  // all lanes active here
         if (lane == 63) {
             red[w * 4 + 0] = cmin;
             red[w * 4 + 1] = bvv;
             red[w * 4 + 2] = __builtin_bit_cast(float, bk);
-            red[w * 4 + 3] = __builtin_bit_cast(float, viol != 0 ? 1u : 0u);
+            red[w * 4 + 3] = __builtin_bit_cast(float, any_viol ? 1u : 0u);
         }
     } else if (lane == 63) {
         red[w * 4 + 0] = kInf;
