@@ -43,8 +43,15 @@ $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS) | $(BUILD)
 $(BUILD)/%.o: $(CSRC)/%.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
 
-$(LIB): $(OBJS)
+$(LIB): $(OBJS) $(BUILD)/pipe.hazards
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+# The pipelined kernel's inline-asm DPP reads rely on the schedule for one of their two wait
+# states: every build checks all of them in the gfx950 code object (tools/dpp_hazards.py).
+$(BUILD)/pipe.hazards: $(BUILD)/pipe.o tools/dpp_hazards.py
+	cd $(BUILD) && /opt/rocm/lib/llvm/bin/llvm-objdump --offloading pipe.o > /dev/null
+	/opt/rocm/lib/llvm/bin/llvm-objdump -d $(BUILD)/pipe.o.0.hipv4-amdgcn-amd-amdhsa--gfx950 > $(BUILD)/pipe.s
+	python3 tools/dpp_hazards.py $(BUILD)/pipe.s pipe_viterbi_kernel > $@
 
 # Oracle: plain C, every add rounded on its own (test infrastructure only).
 $(ORACLE): oracle/viterbi_oracle.c oracle/viterbi_oracle.h

@@ -76,8 +76,12 @@ __device__ __forceinline__ void chain_terms(float& xb, float& xa, float eb, floa
 }
 
 // The same with lane 0's chain input taken from lane R of the group vector bvv (row_ror:16-R
-// rotates lane R of each row of 16 into its lane 0; no SGPR round trip).  xa comes first and an s_nop follows, so both DPP sources have two wait
-// states after whatever wrote them last.
+// rotates lane R of each row of 16 into its lane 0; no SGPR round trip).  xa comes first, so x
+// has its two wait states inside the block; bvv has one inside the block and gets the other from
+// the schedule around it (bvv is written at the start of a group, never by the instruction before
+// a step).  The compiler does not see DPP inside asm, so the build checks every DPP read of the
+// kernel for the two wait states (tools/dpp_hazards.py, Makefile); the s_nop the block carried
+// before cost 1.6 % (A/B 0.361 vs 0.367 ms).
 template <int R>
 __device__ __forceinline__ void chain_terms_v(float& xb, float& xa, float eb, float ea, float bvv, float f,
                                               float x) {
@@ -89,7 +93,6 @@ __device__ __forceinline__ void chain_terms_v(float& xb, float& xa, float eb, fl
             : "v"(bvv), "v"(eb), "v"(f), "v"(ea), "v"(x));
     } else {
         asm("v_add_f32_e32 %1, %4, %5\n\t"
-            "s_nop 0\n\t"
             "v_add_f32_dpp %0, %2, %3 row_ror:%7 row_mask:0xf bank_mask:0xf\n\t"
             "v_add_f32_dpp %0, %6, %3 wave_shr:1 row_mask:0xf bank_mask:0xf"
             : "=&v"(xb), "=&v"(xa)
@@ -474,9 +477,18 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 float bv_next = kInf;
                 bool next_ok = false;
                 if constexpr (SRC == 1) bv_next = ring_prev[(lane & 7u) * 64 + 63];  // group at t (t % 32 == 0)
-                for (; t + 32 <= len; t += 32) {
+                while (t + 32 <= len) {
+                  // the window of t, loaded and waited for here (an asm use), so no load of it is
+                  // pending inside the iterations: the compiler would otherwise wait for every
+                  // vector-memory operation (granule prefetches and stores included) before each
+                  // iteration's reads of the window
+                  cwi = t >> 10;
+                  cw = load_window(cwi);
+                  asm volatile("" ::"v"(cw.x), "v"(cw.y), "v"(cw.z), "v"(cw.w));
+                  spins = spins > kSpinLimit ? spins : 0u;  // new window, new budget (a give-up sticks)
+                  const uint32_t wend = (cwi + 1) << 10;
+                  for (; t + 32 <= len && t < wend; t += 32) {
                     if (dbg) ++dg[7];
-                    window_for(t);
                     const uint32_t r = t & 1023u, ln = r >> 4;
                     const uint64_t sw0 = (uint64_t)readlane_u(cw.x, ln) | ((uint64_t)readlane_u(cw.y, ln) << 32);
                     const uint64_t sw1 = (uint64_t)readlane_u(cw.z, ln) | ((uint64_t)readlane_u(cw.w, ln) << 32);
@@ -567,7 +579,12 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                     group(std::integral_constant<uint32_t, 1>{}, sw1);
                     group(std::integral_constant<uint32_t, 2>{}, sw2);
                     group(std::integral_constant<uint32_t, 3>{}, sw3);
+                  }
                 }
+                // the tail's windows
+                cwi = t >> 10;
+                cw = load_window(cwi);
+                nw = load_window(cwi + 1);
                 bprev = readlane_f(bv_prev, 7);
                 if constexpr (SRC == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the prefetches
                 if constexpr (DST == 2) {

@@ -1,21 +1,20 @@
-// Decoded paths of the pipelined latency plan (pipe.hip PATHS): heavy records, then the path walk.
+// Decoded paths of the pipelined latency plan (pipe.hip PATHS): the path walk.
 //
 // Reference semantics: the oracle's backpointer of state j at observation t is the lexicographic
 // (value, row) argmin over row j's terms of GraphBLAS_impl.cpp:64-73's product
 // min_k fl(fl(E[o][j] + T^T[j][k]) + v[k]) (viterbi_oracle.c step / ora_traceback; lowest row on
 // ties, a term that exists with weight +inf still counts).  The kernel records, per light
-// position and observation, whether F's term was taken (mask words); this kernel rebuilds the
-// heavy rows' inputs per observation -- F's and S's scores and the light minimum mu -- from the
-// kernel's per-block partials, and walks each path back from its best final state:
-//   * records rec[r] = {F(r), C(r), mu(r)} for r in [0, len-1) (all threads of the workgroup):
+// position and observation, whether F's term was taken (mask words); the heavy rows' inputs of an
+// observation -- F's and S's scores and the light minimum mu -- are rebuilt where the walk needs
+// them from the kernel's per-block partials (RecSrc):
 //       mu(r) = min over blocks and half-waves of prec[.][.][r+1].x   (exact: min is exact)
 //       C(r)  = min over blocks and half-waves of prec[.][.][r].y, C(0) = fl(E_S(o_0) + start_S)
 //       F(r)  = F(32k) from fck, advanced by F = fl(X_FF(o_i) + F) (the kernel's speculated F,
 //               exact for every row the kernel did not flag)
-//   * the walk (one wave): as chain_paths.hip's chain_traceback_kernel -- speculative along light
-//     runs and heavy self-loop runs, 64 observations per round -- with the pipelined plan's
-//     layouts; where a heavy row's light-set term wins or ties, the lowest light position j* with
-//     fl(cA + v[j]) == fl(cA + mu) is recomputed from the light checkpoint below that row.
+// The walk (one wave per sequence) is chain_paths.hip's chain_traceback_kernel -- speculative
+// along light runs and heavy self-loop runs, 64 observations per round -- with the pipelined
+// plan's layouts; where a heavy row's light-set term wins or ties, the lowest light position j*
+// with fl(cA + v[j]) == fl(cA + mu) is recomputed from the light checkpoint below that row.
 #include "pipe_common.h"
 
 namespace svh {
@@ -25,44 +24,91 @@ using namespace pipe_dev;
 
 namespace {
 
-constexpr uint32_t kPTbThreads = 256;
 constexpr uint32_t kPTbMaxP = 2560;  // light positions the j* recompute stages in LDS (x2 buffers)
+constexpr uint32_t kPTbMaxN = kPTbMaxP + 2;  // states whose position map is staged in LDS
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
+// The heavy rows' inputs of record row r (observation r+1), rebuilt on demand from the kernel's
+// per-block partials (prec[u][t] = {mu_u(t-1), C_u(t)}, u over blocks x half-waves) and F's
+// 32-observation checkpoints: min is exact, and F is re-advanced with the kernel's own
+// fl(X_FF(o) + F).
+struct RecSrc {
+    const float2* prec;
+    const float* fck;
+    const uint8_t* sym;
+    const float* hcl;  // [S][8] heavy constants (LDS)
+    uint32_t len, U;
+    float c0;          // C(0) = fl(E_S(o_0) + start_S)
+    __device__ float F(uint32_t r) const {
+        const uint32_t r0 = r & ~31u;
+        float xf[31];
+#pragma unroll
+        for (int i = 0; i < 31; ++i) xf[i] = r0 + 1 + i <= r ? hcl[(size_t)sym[r0 + 1 + i] * 8 + 3] : 0.0f;
+        float f = fck[r0 >> 5];
+#pragma unroll
+        for (int i = 0; i < 31; ++i)
+            if (r0 + 1 + i <= r) f = xf[i] + f;
+        return f;
+    }
+    // which = 0: mu(r) (the .x of observation r+1), 1: C(r) (the .y of observation r)
+    __device__ float reduce(uint32_t t, int which) const {
+        float acc = kInf;
+        uint32_t u = 0;
+        for (; u + 8 <= U; u += 8) {
+            float x[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float2 e = prec[(size_t)(u + k) * len + t];
+                x[k] = which ? e.y : e.x;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc = fminf(acc, x[k]);
+        }
+        for (; u < U; ++u) {
+            const float2 e = prec[(size_t)u * len + t];
+            acc = fminf(acc, which ? e.y : e.x);
+        }
+        return acc;
+    }
+    __device__ float mu(uint32_t r) const { return reduce(r + 1, 0); }
+    __device__ float C(uint32_t r) const { return r ? reduce(r, 1) : c0; }
+};
+
 // j* of record row r for heavy row h (0 = F, 1 = S): the lowest light position p with
 // fl(cA_h + v_r[p]) == fl(cA_h + mu_r), cA_h the light-set constant of h for the symbol of
 // observation r+1.  v_r is recomputed by one wave from the checkpoint row c = r rounded down to
 // kCkptEvery with the kernel's float operations: v_i[p] = fminf(fl(ea_p + F(i-1)),
-// fl(eb_p + v_{i-1}[p-1])) (v_{i-1}[-1] = +inf), F(i-1) from the records.
-__device__ uint32_t pipe_jstar(const PipeModel& m, const uint8_t* sym, const float* ck, const float4* rec,
-                               uint32_t r, uint32_t h, float* buf) {
+// fl(eb_p + v_{i-1}[p-1])) (v_{i-1}[-1] = +inf), F advanced alongside from F(c).
+__device__ uint32_t pipe_jstar(const PipeModel& m, const RecSrc& rs, const float* ck, uint32_t r, uint32_t h,
+                               float* buf) {
     const uint32_t lane = threadIdx.x & 63u, P = m.P, SM = m.SM, bsz = 64 * SM;
     const uint32_t c = r / kCkptEvery * kCkptEvery;
     float* cur = buf;
     float* nxt = buf + kPTbMaxP;
     const float* ckr = ck + (size_t)(c / kCkptEvery) * P;
     for (uint32_t x = lane; x < P; x += 64) cur[x] = ckr[x];
+    float F = rs.F(c);
     wave_sync();
     for (uint32_t i = c + 1; i <= r; ++i) {
-        const uint32_t o = sym[i];
-        const float F = rec[i - 1].x;
+        const uint32_t o = rs.sym[i];
         for (uint32_t x = lane; x < P; x += 64) {
             const uint32_t blk = x / bsz, ln = (x % bsz) / SM, s = x % SM;
             const float2 e = m.tab[(((size_t)blk * m.S + o) * SM + s) * 64 + ln];
             const float pv = x ? cur[x - 1] : kInf;
             nxt[x] = fminf(e.y + F, e.x + pv);
         }
+        F = rs.hcl[(size_t)o * 8 + 3] + F;  // F(i)
         wave_sync();
         float* t = cur;
         cur = nxt;
         nxt = t;
     }
-    const float mu = rec[r].z;
-    const float ca = m.hc[(size_t)sym[r + 1] * 8 + (h == 0 ? 1 : 0)];  // A_F or A_S
+    const float mu = rs.mu(r);
+    const float ca = rs.hcl[(size_t)rs.sym[r + 1] * 8 + (h == 0 ? 1 : 0)];  // A_F or A_S
     const float tgt = ca + mu;
     uint32_t best = 0xFFFFFFFFu;
     for (uint32_t x = lane; x < P; x += 64)
@@ -72,46 +118,42 @@ __device__ uint32_t pipe_jstar(const PipeModel& m, const uint8_t* sym, const flo
     return best;
 }
 
-__global__ __launch_bounds__(kPTbThreads) void pipe_traceback_kernel(PipeModel m, FusedBatch b, const uint64_t* path_off,
-                                                                      int32_t* paths, const uint32_t* skip) {
+// One wave per sequence.  The walk is chain_paths.hip's: speculative along light runs and heavy
+// self-loop runs, 64 observations per round.  Where the path is in F and F's self loop exists and
+// its row is below every light row, the kernel's exact speculation check (no light term of F ever
+// below its self term on a row this kernel traces) already decides F's backpointer: itself, with
+// no loads; S (and F otherwise) rebuild their inputs on demand (RecSrc).
+__global__ __launch_bounds__(64) void pipe_traceback_kernel(PipeModel m, FusedBatch b, const uint64_t* path_off,
+                                                             int32_t* paths, const uint32_t* skip) {
     __shared__ float buf[2 * kPTbMaxP];
-    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+    // the walk's per-round lookups, staged in LDS (the masks, partials and symbols of a round's
+    // 64 observations are its only global loads)
+    __shared__ float hcl[32 * 8];
+    __shared__ int32_t sposl[kPTbMaxN];
+    __shared__ uint32_t lrowl[kPTbMaxP];
+    __shared__ uint8_t pfl[kPTbMaxP];
+    const uint32_t q = blockIdx.x, lane = threadIdx.x;
     if (skip && skip[q]) return;  // re-run (and traced) by the chain kernel
+    for (uint32_t x = lane; x < m.S * 8; x += 64) hcl[x] = m.hc[x];
+    for (uint32_t x = lane; x < m.n; x += 64) sposl[x] = m.spos[x];
+    for (uint32_t x = lane; x < m.P; x += 64) {
+        lrowl[x] = m.lrow[x];
+        pfl[x] = m.pflags[x];
+    }
     const uint32_t len = b.end[q];
     const uint32_t nblk = m.nblk, SM = m.SM, bsz = 64 * SM;
-    const uint8_t* sym = b.symbols + b.sym_off[q];
-    const float2* prec = b.prec + b.prec_off[q];
-    const float* fck = b.fck + b.fck_off[q];
-    float4* rec = reinterpret_cast<float4*>(b.hrec + b.hrec_off[q]);
-    const uint32_t rows = len - 1;
+    RecSrc rs;
+    rs.prec = b.prec + b.prec_off[q];
+    rs.fck = b.fck + b.fck_off[q];
+    rs.sym = b.symbols + b.sym_off[q];
+    rs.hcl = hcl;
+    rs.len = len;
+    rs.U = 2 * nblk;
+    wave_sync();
+    rs.c0 = m.rowS >= 0 ? hcl[(size_t)rs.sym[0] * 8 + 6] + m.startS : kInf;
+    // F's backpointer is itself wherever the kernel's check held (see above)
+    const bool f_self = ((m.hx_exist & 1u) != 0) && (!(m.hl_exist & 1u) || (uint32_t)m.rowF < lrowl[0]);
 
-    // ---- records
-    for (uint32_t r = tid; r < rows; r += kPTbThreads) {
-        float mu = kInf, C = kInf;
-        for (uint32_t u = 0; u < 2 * nblk; ++u) {
-            const float2* pu = prec + (size_t)u * len;
-            mu = fminf(mu, pu[r + 1].x);
-            if (r) C = fminf(C, pu[r].y);
-        }
-        if (r == 0) C = m.rowS >= 0 ? m.hc[(size_t)sym[0] * 8 + 6] + m.startS : kInf;
-        float* rw = reinterpret_cast<float*>(rec + r);
-        rw[1] = C;
-        rw[2] = mu;
-    }
-    for (uint32_t k = tid; k * 32 < rows; k += kPTbThreads) {
-        float F = fck[k];
-        const uint32_t r1 = min(rows, k * 32 + 32);
-        reinterpret_cast<float*>(rec + k * 32)[0] = F;
-        for (uint32_t r = k * 32 + 1; r < r1; ++r) {
-            F = m.hc[(size_t)sym[r] * 8 + 3] + F;  // fl(X_FF(o_r) + F(r-1))
-            reinterpret_cast<float*>(rec + r)[0] = F;
-        }
-    }
-    __syncthreads();
-    if (tid >= 64) return;
-
-    // ---- walk (one wave)
-    const uint32_t lane = tid;
     const uint32_t* msk = b.cmask + b.cmask_off[q];
     const float* ck = b.ckpt + b.ckpt_off[q];
     const uint32_t wstride = nblk * SM * 64;
@@ -126,7 +168,7 @@ __global__ __launch_bounds__(kPTbThreads) void pipe_traceback_kernel(PipeModel m
             for (int64_t r = lane; r < i; r += 64) out[r] = -1;
             break;
         }
-        const int32_t pos = m.spos[s];
+        const int32_t pos = sposl[s];
         const int64_t r = i - 1 - (int64_t)lane;  // record row of this lane (observation r+1)
         const bool valid = r >= 0;
         int32_t pred = -1;
@@ -139,29 +181,30 @@ __global__ __launch_bounds__(kPTbThreads) void pipe_traceback_kernel(PipeModel m
             if (valid && p >= 0) {
                 const uint32_t pp = (uint32_t)p, blk = pp / bsz, ln = (pp % bsz) / SM, ss = pp % SM;
                 const uint32_t word = msk[((uint64_t)r >> 5) * wstride + (blk * SM + ss) * 64 + ln];
-                const uint32_t f = m.pflags[pp];
+                const uint32_t f = pfl[pp];
                 if ((word >> (31u - ((uint32_t)r & 31u))) & 1u) {
                     pred = m.rowF;
                 } else if ((f & 1u) && pp >= 1) {
-                    pred = (int32_t)m.lrow[pp - 1];
+                    pred = (int32_t)lrowl[pp - 1];
                     cont = true;
                 }
             }
+        } else if (valid && pos == -1 && f_self) {  // F's self loop (the kernel's check decided it)
+            pred = m.rowF;
+            cont = pred == s;
         } else if (valid) {  // heavy run: self-loops of heavy row h
             // the heavy row's lexicographic (value, row) argmin at observation r+1, re-evaluated
-            // from the records with the kernel's float operations: heavy terms fl(cX + vo[k]) and
-            // the light-set term fl(cA + mu)
+            // from its rebuilt inputs with the kernel's float operations: heavy terms fl(cX + vo[k])
+            // and the light-set term fl(cA + mu)
             const uint32_t h = (uint32_t)(-1 - pos);
-            const float4 rw = rec[r];
-            const float vo[2] = {rw.x, rw.y};
-            const float mu = rw.z;
-            const float* hc = m.hc + (size_t)sym[r + 1] * 8;  // A_S A_F X_SS X_FF X_SF
+            const uint32_t rr = (uint32_t)r;
+            const float* hc = hcl + (size_t)rs.sym[rr + 1] * 8;  // A_S A_F X_SS X_FF X_SF
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 if ((m.hx_exist >> (h * 2 + k)) & 1u) {
                     // X[h][k]: F <- F = X_FF, S <- F = X_SF, S <- S = X_SS (F <- S never: plan)
                     const float cx = h == 0 ? hc[3] : (k == 0 ? hc[4] : hc[2]);
-                    const float val = cx + vo[k];
+                    const float val = cx + (k == 0 ? rs.F(rr) : rs.C(rr));
                     const uint32_t col = (uint32_t)hrowk[k];
                     const bool take = !hex || val < hv || (val == hv && col < hcol);
                     hv = take ? val : hv;
@@ -171,7 +214,7 @@ __global__ __launch_bounds__(kPTbThreads) void pipe_traceback_kernel(PipeModel m
             }
             pred = hex ? (int32_t)hcol : -1;
             if ((m.hl_exist >> h) & 1u) {
-                lv = hc[h == 0 ? 1 : 0] + mu;
+                lv = hc[h == 0 ? 1 : 0] + rs.mu(rr);
                 needj = !hex || !(hv < lv);  // the light set wins or ties: its lowest row j* decides
             }
             cont = !needj && pred == s;
@@ -179,10 +222,10 @@ __global__ __launch_bounds__(kPTbThreads) void pipe_traceback_kernel(PipeModel m
         uint64_t stop = __builtin_amdgcn_ballot_w64(!cont);
         uint32_t ls = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;  // first lane leaving the run
         while (ls < 64u && __builtin_amdgcn_readlane((int)needj, (int)ls)) {
-            const uint32_t rs = (uint32_t)(i - 1 - (int64_t)ls);
-            const uint32_t jp = pipe_jstar(m, sym, ck, rec, rs, (uint32_t)(-1 - pos), buf);
+            const uint32_t rj = (uint32_t)(i - 1 - (int64_t)ls);
+            const uint32_t jp = pipe_jstar(m, rs, ck, rj, (uint32_t)(-1 - pos), buf);
             if (lane == ls) {
-                const uint32_t js = jp == 0xFFFFFFFFu ? 0xFFFFFFFFu : m.lrow[jp];
+                const uint32_t js = jp == 0xFFFFFFFFu ? 0xFFFFFFFFu : lrowl[jp];
                 const uint32_t k = !hex || lv < hv ? js : min(hcol, js);
                 pred = k == 0xFFFFFFFFu ? -1 : (int32_t)k;
                 cont = pred == s;
@@ -203,11 +246,11 @@ __global__ __launch_bounds__(kPTbThreads) void pipe_traceback_kernel(PipeModel m
 
 hipError_t launch_pipe_traceback(const PipeModel& m, const FusedBatch& b, const uint64_t* path_off, int32_t* paths,
                                  const uint32_t* skip, hipStream_t stream) {
-    if (!b.cmask || !b.hrec || !b.ckpt || !b.prec || !b.fck || !m.pflags || !m.spos || m.P > kPTbMaxP ||
+    if (!b.cmask || !b.ckpt || !b.prec || !b.fck || !m.pflags || !m.spos || m.P > kPTbMaxP || m.n > kPTbMaxN ||
         m.S > 32)
         return hipErrorInvalidValue;
     if (b.nseq == 0) return hipSuccess;
-    hipLaunchKernelGGL(pipe_traceback_kernel, dim3(b.nseq), dim3(kPTbThreads), 0, stream, m, b, path_off, paths, skip);
+    hipLaunchKernelGGL(pipe_traceback_kernel, dim3(b.nseq), dim3(64), 0, stream, m, b, path_off, paths, skip);
     return hipGetLastError();
 }
 
