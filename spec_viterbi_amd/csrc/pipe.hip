@@ -49,6 +49,27 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr uint32_t kR = kPipeRing;
 
+// Granule hand-off between workgroups: groups of 8 granules the consumer keeps in flight ahead of
+// use (1, 2 or 4), and the step of the next group at which the producer stores a finished group's
+// granules (0: at the end of the next group).  A/B knobs (tools/ab_build.sh -D...).
+#ifndef SVH_PIPE_GPF
+#define SVH_PIPE_GPF 2
+#endif
+#ifndef SVH_PIPE_GST
+#define SVH_PIPE_GST 2
+#endif
+constexpr uint32_t kGpf = SVH_PIPE_GPF;
+constexpr uint32_t kGst = SVH_PIPE_GST;
+static_assert(kGpf == 1 || kGpf == 2 || kGpf == 4, "granule prefetch depth");
+static_assert(kGst < 8, "granule store step");
+
+template <uint32_t N>
+__device__ __forceinline__ void wait_vmcnt() {
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+}
+
 // One lane's LDS store of a wave-uniform word: EXEC narrowed to lane 0 inside the asm (no
 // divergent branch in the compiler's view).
 __device__ __forceinline__ void lds_put1(uint32_t addr, uint32_t v) {
@@ -145,9 +166,19 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     float last_pm = kInf;
     // diagnostics: 0 loop cycles, 1 head cycles, 2 tail cycles, 3 slow re-reads waiting for the
     // previous wave, 4 ... for the next wave (flow control), 5 ... for granules, 6 ... for the
-    // consumer's progress word, 7 body iterations
+    // consumer's progress word, 7 body iterations, 8 .. 11 the 100 MHz real-time clock at wave
+    // entry, sweep start, body end, sweep end.  Built only with -DSVH_PIPE_DIAG (tools/ab_build.sh;
+    // then SVH_PIPE_DEBUG=1 at run time): the counters would otherwise hold SGPRs through the loop
+    // in the production kernel, whose SGPRs are its scarcest register file.
     unsigned long long dg[kPipeStamps] = {};
+#ifdef SVH_PIPE_DIAG
     const bool dbg = m.stamps != nullptr;
+#define SVH_RT(k) (dg[k] = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull)
+#else
+    constexpr bool dbg = false;
+#define SVH_RT(k) ((void)0)
+#endif
+    SVH_RT(8);
 
     if (act) {
         const uint32_t p0 = blk * 64 * SM + lane * SM;
@@ -262,16 +293,47 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 
         // ---- symbols: 1024-observation windows in VGPRs (lane l: bytes 16l..16l+15)
         const uint32_t slen = len + kSymPad;
-        auto load_window = [&](uint32_t wi) -> uint4 {
-            const uint32_t off = wi * kPipeWindow + lane * 16;
-            return off < slen ? *reinterpret_cast<const uint4*>(sym + off) : make_uint4(0, 0, 0, 0);
+        // Observations run in groups of 32 aligned to `first` (tb = first % 32; 0 for the path
+        // variants, whose records sit at absolute multiples of 32): the body starts at first
+        // itself, with no head of single observations (each one an LDS or L2 round trip, and the
+        // head's cost adds up along the chain of waves).  What is indexed by the position in the
+        // cycle of 32 -- symbol windows, LDS ring slots -- uses u = t - tb; counts, granules and
+        // tags use t.
+#ifdef SVH_PIPE_HEAD  // A/B diagnostic: the head of single observations of before
+        const uint32_t tb = 0u;
+#else
+        const uint32_t tb = PATHS ? 0u : (first & 31u);
+#endif
+        auto load_window = [&](uint32_t wi) -> uint4 {  // lane l: symbols of u = 1024 wi + 16 l ..
+            const uint32_t off = wi * kPipeWindow + lane * 16 + tb;
+            if ((tb & 15u) == 0)
+                return off < slen ? *reinterpret_cast<const uint4*>(sym + off) : make_uint4(0, 0, 0, 0);
+            // unaligned: two aligned 16-byte loads and a byte funnel shift (once per window)
+            const uint32_t a = off & ~15u, ws = (tb & 15u) >> 2, bs = tb & 3u;
+            const uint4 c0 = a < slen ? *reinterpret_cast<const uint4*>(sym + a) : make_uint4(0, 0, 0, 0);
+            const uint4 c1 = a + 16 < slen ? *reinterpret_cast<const uint4*>(sym + a + 16) : make_uint4(0, 0, 0, 0);
+            auto pick = [&](uint32_t i) -> uint32_t {  // word ws + i of c0 | c1 (selects, no scratch)
+                const uint32_t k = ws + i;
+                uint32_t r = c0.x;
+                r = k == 1 ? c0.y : r;
+                r = k == 2 ? c0.z : r;
+                r = k == 3 ? c0.w : r;
+                r = k == 4 ? c1.x : r;
+                r = k == 5 ? c1.y : r;
+                r = k == 6 ? c1.z : r;
+                r = k == 7 ? c1.w : r;
+                return r;
+            };
+            const uint32_t p0 = pick(0), p1 = pick(1), p2 = pick(2), p3 = pick(3), p4 = pick(4);
+            return make_uint4(__builtin_amdgcn_alignbyte(p1, p0, bs), __builtin_amdgcn_alignbyte(p2, p1, bs),
+                              __builtin_amdgcn_alignbyte(p3, p2, bs), __builtin_amdgcn_alignbyte(p4, p3, bs));
         };
-        uint32_t cwi = first >> 10;
+        uint32_t cwi = (first - tb) >> 10;
         uint4 cw = load_window(cwi), nw = load_window(cwi + 1);
         // The wait budget is per window: a new window resets a healthy counter (a give-up sticks),
         // so no sequence length exhausts it while a stuck wait still gives up within one budget.
         auto window_for = [&](uint32_t t) {  // uniform; windows advance one at a time
-            if ((t >> 10) != cwi) {
+            if (((t - tb) >> 10) != cwi) {
                 cw = nw;
                 ++cwi;
                 nw = load_window(cwi + 1);
@@ -279,7 +341,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             }
         };
         auto sym1 = [&](uint32_t t) -> uint32_t {  // symbol of observation t (slow path)
-            const uint32_t r = t & 1023u, ln = r >> 4, d = (r >> 2) & 3u;
+            const uint32_t r = (t - tb) & 1023u, ln = r >> 4, d = (r >> 2) & 3u;
             const uint32_t wd = d == 0 ? readlane_u(cw.x, ln) : d == 1 ? readlane_u(cw.y, ln)
                               : d == 2 ? readlane_u(cw.z, ln) : readlane_u(cw.w, ln);
             return (wd >> ((r & 3u) * 8)) & 0xFFu;
@@ -362,16 +424,28 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 __builtin_amdgcn_s_sleep(1);
             }
         };
-        auto gran_value = [&](uint32_t s) -> float {  // poll the granule of observation s (uniform)
-            const uint64_t* p = gin + (s & (kGR - 1));
-            uint64_t gv = g_ld64(p);
-            while ((uint32_t)uniform((int)(uint32_t)(gv >> 32)) != gtag(ep, s)) {
-                if (dbg) ++dg[5];
-                if (give_up()) break;
-                __builtin_amdgcn_s_sleep(1);
-                gv = g_ld64(p);
+        // The boundary score of observation s from the previous workgroup's granules (uniform), for
+        // the single observations (the tail, the path variants' head): eight granules per poll
+        // (lanes 0..7: s .. s+7), one L2 round trip per 8 observations instead of one each.
+        // Only granules this wave reads (observations <= len-2) are awaited.
+        float gvec = 0.0f;
+        uint32_t gbase = 0x80000000u;  // no observation index reaches it: the first call loads
+        auto gran_single = [&](uint32_t s) -> float {
+            if (s - gbase >= 8u) {
+                gbase = s;
+                const uint32_t sl = s + (lane & 7u);
+                const bool need = lane < 8u && sl + 1u < len;
+                const uint64_t* p = gin + (sl & (kGR - 1));
+                uint64_t gv = g_ld64(p);
+                while (__builtin_amdgcn_ballot_w64(need && (uint32_t)(gv >> 32) != gtag(ep, sl)) != 0) {
+                    if (dbg) ++dg[5];
+                    if (give_up()) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    gv = g_ld64(p);
+                }
+                gvec = __builtin_bit_cast(float, (uint32_t)gv);
             }
-            return __builtin_bit_cast(float, (uint32_t)uniform((int)(uint32_t)gv));
+            return readlane_f(gvec, s - gbase);
         };
         auto cons_ok = [&](uint64_t c, uint32_t need) -> bool {  // consumer progress word vs need
             return (uint32_t)(c >> 32) == ep && (int)(uint32_t)c >= (int)need;
@@ -392,7 +466,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             const uint64_t gv = ((uint64_t)gtag(ep, s) << 32) | __builtin_bit_cast(uint32_t, val);
             if (lane == 0) g_st64(gout + (s & (kGR - 1)), gv);
         };
-        auto ring_put = [&](uint32_t t, float val) { ring_w[(t & (kR - 1)) * 64 + lane] = val; };
+        auto ring_put = [&](uint32_t t, float val) { ring_w[((t - tb) & (kR - 1)) * 64 + lane] = val; };
 
         // The sweep, with the boundary roles as compile-time constants (one code path per role).
         auto sweep = [&](auto srcc, auto dstc) {
@@ -415,9 +489,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                     if constexpr (SRC == 1) {
                         wait_prev(t + 1);
                         asm volatile("" ::: "memory");
-                        bprev = readlane_f(ring_prev[(t & (kR - 1)) * 64 + 63], 0);
+                        bprev = readlane_f(ring_prev[((t - tb) & (kR - 1)) * 64 + 63], 0);
                     } else if constexpr (SRC == 2) {
-                        bprev = gran_value(t);
+                        bprev = gran_single(t);
                     }
                 }
                 asm volatile("" ::: "memory");
@@ -435,19 +509,21 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             if constexpr (SRC == 1) {
                 wait_prev(first);
                 asm volatile("" ::: "memory");
-                bprev = readlane_f(ring_prev[((first - 1) & (kR - 1)) * 64 + 63], 0);
+                bprev = readlane_f(ring_prev[((first - 1 - tb) & (kR - 1)) * 64 + 63], 0);
             } else if constexpr (SRC == 2) {
-                bprev = gran_value(first - 1);
-                // initial progress (observations < first are done): a row that starts mid-sequence
-                // at a multiple of 64 would otherwise leave its producer's first flow-control wait
-                // on a stale word while this wave waits for that producer's granules
+                // initial progress (observations < first are done), published before the first
+                // poll: a row that starts mid-sequence at a multiple of 64 would otherwise leave its
+                // producer's first flow-control wait on a stale word while this wave waits for that
+                // producer's granules (the poll awaits observations up to first+6)
                 if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | first);
+                bprev = gran_single(first - 1);
             }
 
             uint32_t t = first;
             unsigned long long c0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
-            // head: single observations up to a multiple of 32
-            for (; t < len && (t & 31u); ++t) single(t);
+            SVH_RT(9);
+            // head: single observations up to the first group of 32 (none unless tb is forced to 0)
+            for (; t < len && ((t - tb) & 31u); ++t) single(t);
             if (dbg) {
                 const unsigned long long c1 = __builtin_amdgcn_s_memtime();
                 dg[1] = c1 - c0;
@@ -456,10 +532,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 
             // body: 32 observations per iteration, four groups of 8
             if (t + 32 <= len) {
-                uint64_t gq[4] = {0, 0, 0, 0};  // SRC 2: granule groups in flight
+                uint64_t gq[kGpf] = {};  // SRC 2: granule groups in flight
                 if constexpr (SRC == 2) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) g_prefetch64(gq[j], gin + ((t + 8 * j + (lane & 7u)) & (kGR - 1)));
+                    for (uint32_t j = 0; j < kGpf; ++j) g_prefetch64(gq[j], gin + ((t + 8 * j + (lane & 7u)) & (kGR - 1)));
                 }
                 float gpend = 0.0f;    // DST 2: the previous group's boundary scores (lanes 0..7),
                 uint32_t gpend_t = 0;  // read back from the ring one group before they are stored
@@ -476,20 +552,20 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 // next_ok) into this one loop-carried register, re-loaded there when it was stale
                 float bv_next = kInf;
                 bool next_ok = false;
-                if constexpr (SRC == 1) bv_next = ring_prev[(lane & 7u) * 64 + 63];  // group at t (t % 32 == 0)
+                if constexpr (SRC == 1) bv_next = ring_prev[(lane & 7u) * 64 + 63];  // group at t (u % 32 == 0)
                 while (t + 32 <= len) {
                   // the window of t, loaded and waited for here (an asm use), so no load of it is
                   // pending inside the iterations: the compiler would otherwise wait for every
                   // vector-memory operation (granule prefetches and stores included) before each
                   // iteration's reads of the window
-                  cwi = t >> 10;
+                  cwi = (t - tb) >> 10;
                   cw = load_window(cwi);
                   asm volatile("" ::"v"(cw.x), "v"(cw.y), "v"(cw.z), "v"(cw.w));
                   spins = spins > kSpinLimit ? spins : 0u;  // new window, new budget (a give-up sticks)
-                  const uint32_t wend = (cwi + 1) << 10;
+                  const uint32_t wend = ((cwi + 1) << 10) + tb;
                   for (; t + 32 <= len && t < wend; t += 32) {
                     if (dbg) ++dg[7];
-                    const uint32_t r = t & 1023u, ln = r >> 4;
+                    const uint32_t r = (t - tb) & 1023u, ln = r >> 4;
                     const uint64_t sw0 = (uint64_t)readlane_u(cw.x, ln) | ((uint64_t)readlane_u(cw.y, ln) << 32);
                     const uint64_t sw1 = (uint64_t)readlane_u(cw.z, ln) | ((uint64_t)readlane_u(cw.w, ln) << 32);
                     const uint64_t sw2 = (uint64_t)readlane_u(cw.x, ln + 1) | ((uint64_t)readlane_u(cw.y, ln + 1) << 32);
@@ -503,8 +579,8 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         const uint32_t tg = t + 8 * j;
                         float bv = kInf;  // lanes 0..7: the previous block's last scores of tg..tg+7
                         if constexpr (SRC == 2) {
-                            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // gq[j]: 3 later loads in flight
-                            uint64_t gv = gq[j];
+                            wait_vmcnt<kGpf - 1>();  // gq[j]: kGpf - 1 later loads in flight
+                            uint64_t gv = gq[j % kGpf];
                             while (__builtin_amdgcn_ballot_w64((uint32_t)(gv >> 32) != gtag(ep, tg)) != 0) {
                                 if (dbg) ++dg[5];
                                 if (give_up()) break;
@@ -512,7 +588,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                 gv = g_ld64(gin + ((tg + (lane & 7u)) & (kGR - 1)));
                             }
                             bv = __builtin_bit_cast(float, (uint32_t)gv);
-                            g_prefetch64(gq[j], gin + ((tg + 32 + (lane & 7u)) & (kGR - 1)));
+                            g_prefetch64(gq[j % kGpf], gin + ((tg + 8 * kGpf + (lane & 7u)) & (kGR - 1)));
                         }
                         if constexpr (DST == 1) {
                             if ((int)uniform((int)nc_rd) < (int)tg + 8 - (int)kR) wait_next((int)tg + 8 - (int)kR);
@@ -546,6 +622,12 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                 if constexpr (SRC == 1) pc_rd = lds_ld32(cnt_w - 1);
                                 if constexpr (DST == 1) nc_rd = lds_ld32(cnt_w + 1);
                             }
+                            if constexpr (DST == 2 && kGst != 0 && k == kGst) {  // the last group's granules
+                                if (gpend_t && lane < 8)
+                                    g_st64(gout + ((gpend_t + lane) & (kGR - 1)),
+                                           ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
+                                gpend_t = 0;
+                            }
                         };
                         one(std::integral_constant<uint32_t, 0>{});
                         one(std::integral_constant<uint32_t, 1>{});
@@ -565,9 +647,11 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         }
                         if constexpr (DST == 2) {
                             // granules of the previous group (read back from the ring one group ago)
-                            if (gpend_t && lane < 8)
-                                g_st64(gout + ((gpend_t + lane) & (kGR - 1)),
-                                       ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
+                            if constexpr (kGst == 0) {
+                                if (gpend_t && lane < 8)
+                                    g_st64(gout + ((gpend_t + lane) & (kGR - 1)),
+                                           ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
+                            }
                             gpend = ring_w[(8 * j + (lane & 7u)) * 64 + 63];
                             gpend_t = tg;
                         }
@@ -581,8 +665,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                     group(std::integral_constant<uint32_t, 3>{}, sw3);
                   }
                 }
-                // the tail's windows
-                cwi = t >> 10;
+                // the tail's windows; the tail's granule polls start afresh (nothing of the head's
+                // stays live through the body)
+                gbase = 0x80000000u;
+                cwi = (t - tb) >> 10;
                 cw = load_window(cwi);
                 nw = load_window(cwi + 1);
                 bprev = readlane_f(bv_prev, 7);
@@ -598,9 +684,11 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 dg[0] = c1 - c0;
                 c0 = c1;
             }
+            SVH_RT(10);
             // tail
             for (; t < len; ++t) single(t);
             if (dbg) dg[2] = __builtin_amdgcn_s_memtime() - c0;
+            SVH_RT(11);
             if constexpr (PATHS) {
                 // rows the loop did not store: masks of rows below len-1 past the last full word,
                 // ring rows of the last partial group of 32

@@ -802,6 +802,37 @@ void DevicePipePlan::report_stamps(uint32_t nseq) const {
                  "prev %.0f/%.0f next %.0f/%.0f gran %.0f/%.0f cons %.0f/%.0f iters %.0f\n",
                  sum[0] / waves, mx[0], sum[1] / waves, mx[1], sum[2] / waves, mx[2], sum[3] / waves, mx[3],
                  sum[4] / waves, mx[4], sum[5] / waves, mx[5], sum[6] / waves, mx[6], sum[7] / waves);
+    {  // wall clock (100 MHz): per wave entry / sweep start / body end / sweep end, from the launch's first entry
+        unsigned long long t0 = ~0ull, tend = 0;
+        for (size_t w = 0; w < waves; ++w)
+            if (h[w * kPipeStamps + 8]) {
+                t0 = std::min(t0, h[w * kPipeStamps + 8]);
+                tend = std::max(tend, h[w * kPipeStamps + 11]);
+            }
+        if (t0 != ~0ull) std::fprintf(stderr, "pipe wall (us from first entry): last sweep end %.2f\n", (tend - t0) * 0.01);
+        // per sequence (tickets q*G .. q*G+G-1): each workgroup's latest entry, w0 start and latest end
+        for (uint32_t q = 0; t0 != ~0ull && q < nseq; ++q) {
+            std::fprintf(stderr, "  seq %u:", q);
+            for (uint32_t g = 0; g < plan.G; ++g) {
+                unsigned long long en = 0, st = 0, ed = 0;
+                for (uint32_t w = 0; w < plan.W; ++w) {
+                    const unsigned long long* r = h.data() + (((size_t)q * plan.G + g) * plan.W + w) * kPipeStamps;
+                    if (!r[8]) continue;
+                    en = std::max(en, r[8] - t0);
+                    if (w == 0) st = r[9] - t0;
+                    ed = std::max(ed, r[11] - t0);
+                }
+                std::fprintf(stderr, " [g%u in %.1f st %.1f end %.1f]", g, en * 0.01, st * 0.01, ed * 0.01);
+            }
+            std::fprintf(stderr, "\n");
+        }
+        for (size_t w = 0; t0 != ~0ull && w < waves; ++w) {
+            const unsigned long long* r = h.data() + w * kPipeStamps;
+            if (!r[8] || w / plan.W >= 2 * plan.G) continue;  // the first two sequences' waves
+            std::fprintf(stderr, "  wave %zu (seq-ticket %zu): entry %.2f start %.2f body_end %.2f end %.2f\n", w % plan.W,
+                         w / plan.W, (r[8] - t0) * 0.01, (r[9] - t0) * 0.01, (r[10] - t0) * 0.01, (r[11] - t0) * 0.01);
+        }
+    }
     for (uint32_t g = 0; g < plan.G; ++g)
         for (uint32_t w = 0; w < plan.W; ++w) {
             const unsigned long long* r = h.data() + ((size_t)g * plan.W + w) * kPipeStamps;
