@@ -121,6 +121,69 @@ __device__ __forceinline__ void chain_terms_v(float& xb, float& xa, float eb, fl
     }
 }
 
+// Table reads of a step (SVH_PIPE_TAB; A/B knob):
+//   0  the compiler's indexed moves: one s_set_gpr_idx block of SM x 2 v_mov (eb, ea of symbol o),
+//      then the adds, and the heavy constants by four v_readlane (the production kernel);
+//   3  (SM = 2, at most kT3Sym symbols) every table and constant read is an M0-indexed operand of
+//      the add that uses it: 13 VALU per step instead of 21, no v_readlane.  Without the exchange a
+//      step is 8 % faster (66 vs 72 ns), in the pipeline 1 % (0.332 vs 0.336 ms): not the default.
+// Measured and not kept (round 3, A/B on 2405 x emit_50): indexed adds through gpr_idx(SRC0) with
+// the DPP pair after the block (0.39 ms), everything but the constants through gpr_idx(SRC1) (0.37),
+// the constants by a broadcast ds_read_b128 a step ahead instead of v_readlane (0.38): an indexed
+// VALU instruction costs more than the move it saves, and a per-step lgkmcnt(0) more than four
+// v_readlane.
+#ifndef SVH_PIPE_TAB
+#define SVH_PIPE_TAB 0
+#endif
+static_assert(SVH_PIPE_TAB == 0 || SVH_PIPE_TAB == 3, "table read mode");
+
+// Slot 0's chain input for a step: R < 0 the uniform boundary b (SGPR, single observations),
+// R = 0 lane 0 of the group vector, R = 1..7 lane R of the group vector (row_ror:16-R).
+template <int R>
+struct ChainIn {
+    static constexpr int value = R;
+    float b;
+};
+
+#define SVH_TAB3_PLAIN "v_add_f32_e32 %[xb0], %[b], v2\n\t"
+#define SVH_TAB3_ROR "v_add_f32_dpp %[xb0], %[b], v2 row_ror:%[r] row_mask:0xf bank_mask:0xf\n\t"
+// Mode 3 (SM = 2, at most kT3Sym symbols): the heavy constants join the tables, so a step has no
+// v_readlane either.  Four pair-interleaved tables (register 2o = the first value of symbol o,
+// 2o + 1 the second), 40 registers each, pinned to v2..v161:
+//   T1 = {eb_0, ea_0}, T2 = {eb_1, ea_1}, T3 = {A_S, A_F}, T4 = {X_SS, X_FF},
+// indexed by M0 = 2o (the symbol windows are loaded pre-doubled).  The heavy pairs are packed
+// adds with an indexed 64-bit src1: {A_S, A_F} + {m, m} and {X_SS, X_FF} + {c, F}.
+constexpr uint32_t kT3Sym = 20;
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+#define SVH_TAB3(FIRST)                                                              \
+    "s_set_gpr_idx_on %[o], gpr_idx(SRC1)\n\t"                                       \
+    "v_add_f32_e32 %[xa0], %[f], v3\n\t"                                             \
+    "v_add_f32_e32 %[xa1], %[f], v43\n\t"                                            \
+    "v_add_f32_e32 %[xb1], %[v0], v42\n\t" FIRST                                     \
+    "v_add_f32_dpp %[xb0], %[x], v2 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"        \
+    "v_pk_add_f32 %[s1], %[pm], v[82:83] op_sel_hi:[0,1]\n\t"                         \
+    "v_pk_add_f32 %[s2], %[cf], v[122:123]\n\t"                                       \
+    "s_set_gpr_idx_off"
+#define SVH_TAB3_OUT \
+    [xa0] "=&v"(xa[0]), [xa1] "=&v"(xa[1]), [xb0] "=&v"(xb[0]), [xb1] "=&v"(xb[1]), [s1] "=&v"(s1), [s2] "=&v"(s2)
+#define SVH_TAB3_IN                                                                                          \
+    [o] "s"(o2), [f] "v"(cf.y), [v0] "v"(v[0]), [x] "v"(v[1]), [pm] "v"(pmv), [cf] "v"(cf), "{v[2:33]}"(TA[0]), \
+        "{v[34:41]}"(TB[0]), "{v[42:73]}"(TA[1]), "{v[74:81]}"(TB[1]), "{v[82:113]}"(TA[2]),                   \
+        "{v[114:121]}"(TB[2]), "{v[122:153]}"(TA[3]), "{v[154:161]}"(TB[3])
+
+template <int R>
+__device__ __forceinline__ void tab_full(float (&xa)[2], float (&xb)[2], f2& s1, f2& s2, uint32_t o2, f2 cf,
+                                         const float (&v)[2], f2 pmv, ChainIn<R> in, const f32x32 (&TA)[4],
+                                         const f32x8 (&TB)[4]) {
+    if constexpr (R < 0) {
+        asm(SVH_TAB3(SVH_TAB3_PLAIN) : SVH_TAB3_OUT : SVH_TAB3_IN, [b] "s"(in.b) : "m0");
+    } else if constexpr (R == 0) {
+        asm(SVH_TAB3(SVH_TAB3_PLAIN) : SVH_TAB3_OUT : SVH_TAB3_IN, [b] "v"(in.b) : "m0");
+    } else {
+        asm(SVH_TAB3(SVH_TAB3_ROR) : SVH_TAB3_OUT : SVH_TAB3_IN, [b] "v"(in.b), [r] "n"(16 - R) : "m0");
+    }
+}
+
 template <int SM, int W, bool SX, int PATHS>
 __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -188,11 +251,37 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         for (int s = 0; s < SM; ++s)
 #pragma unroll
             for (int o = 0; o < 32; ++o) {
-                const float2 e = (uint32_t)o < S ? m.tab[((size_t)(blk * S + o) * SM + s) * 64 + lane]
-                                                 : make_float2(kInf, kInf);
-                EB[s][o] = e.x;
-                EA[s][o] = e.y;
+                // unconditional loads (a clamped symbol), then a select: all 32 x SM loads go out
+                // back to back (a conditional load per symbol serialised them: ~15 us of prologue)
+                const uint32_t oc = (uint32_t)o < S ? (uint32_t)o : S - 1u;
+                const float2 e = m.tab[((size_t)(blk * S + oc) * SM + s) * 64 + lane];
+                EB[s][o] = (uint32_t)o < S ? e.x : kInf;
+                EA[s][o] = (uint32_t)o < S ? e.y : kInf;
             }
+        // mode 3: the pair-interleaved tables (symbols >= S: +inf)
+        constexpr bool kT3 = SVH_PIPE_TAB == 3 && SM == 2;
+        f32x32 TA[4];
+        f32x8 TB[4];
+        if constexpr (kT3) {
+#pragma unroll
+            for (int o = 0; o < (int)kT3Sym; ++o) {
+                const bool ok = (uint32_t)o < S;
+                const uint32_t oc = ok ? (uint32_t)o : S - 1u;  // unconditional loads, then selects
+                const float2 e0 = m.tab[((size_t)(blk * S + oc) * SM + 0) * 64 + lane];
+                const float2 e1 = m.tab[((size_t)(blk * S + oc) * SM + 1) * 64 + lane];
+                const float4 h = *reinterpret_cast<const float4*>(m.hc + oc * 8);
+                const float val[4][2] = {{ok ? e0.x : kInf, ok ? e0.y : kInf}, {ok ? e1.x : kInf, ok ? e1.y : kInf},
+                                         {ok ? h.x : kInf, ok ? h.y : kInf}, {ok ? h.z : kInf, ok ? h.w : kInf}};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int r = 2 * o + u;
+                        if (r < 32) TA[k][r] = val[k][u];
+                        else TB[k][r - 32] = val[k][u];
+                    }
+            }
+        }
         // heavy constants as lane tables (lane o: symbol o), extracted with v_readlane
         const bool lo = lane < S;
         const float cAS = lo ? m.hc[lane * 8 + 0] : kInf, cAF = lo ? m.hc[lane * 8 + 1] : kInf;
@@ -304,7 +393,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 #else
         const uint32_t tb = PATHS ? 0u : (first & 31u);
 #endif
-        auto load_window = [&](uint32_t wi) -> uint4 {  // lane l: symbols of u = 1024 wi + 16 l ..
+        auto load_window_raw = [&](uint32_t wi) -> uint4 {  // lane l: symbols of u = 1024 wi + 16 l ..
             const uint32_t off = wi * kPipeWindow + lane * 16 + tb;
             if ((tb & 15u) == 0)
                 return off < slen ? *reinterpret_cast<const uint4*>(sym + off) : make_uint4(0, 0, 0, 0);
@@ -328,6 +417,11 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             return make_uint4(__builtin_amdgcn_alignbyte(p1, p0, bs), __builtin_amdgcn_alignbyte(p2, p1, bs),
                               __builtin_amdgcn_alignbyte(p3, p2, bs), __builtin_amdgcn_alignbyte(p4, p3, bs));
         };
+        auto load_window = [&](uint32_t wi) -> uint4 {  // mode 3: every symbol byte doubled (2o < 64)
+            const uint4 w4 = load_window_raw(wi);
+            if constexpr (kT3) return make_uint4(w4.x << 1, w4.y << 1, w4.z << 1, w4.w << 1);
+            return w4;
+        };
         uint32_t cwi = (first - tb) >> 10;
         uint4 cw = load_window(cwi), nw = load_window(cwi + 1);
         // The wait budget is per window: a new window resets a healthy counter (a give-up sticks),
@@ -348,33 +442,64 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         };
 
         // ---- one observation with symbol o; bnd = the previous block's last score at t-1
-        auto step = [&](uint32_t o, auto chain) {
+        // `in`: ChainIn<R>, slot 0's chain input (see ChainIn)
+        auto step = [&](uint32_t o, auto in) {
+            constexpr int R = decltype(in)::value;
+            float xa[SM], xb[SM];  // feeder and chain terms of every slot
+            if constexpr (kT3) {  // o is 2 x the symbol
+                float vv[2] = {v[0], v[SM - 1]};
+                float xa2[2], xb2[2];
+                f2 pmv;
+                pmv.x = fminf(v[0], v[SM - 1]);
+                f2 s1, s2;
+                tab_full<R>(xa2, xb2, s1, s2, o, CF, vv, pmv, ChainIn<R>{in.b}, TA, TB);
+                float cn = fminf(s1.x, s2.x);
+                if constexpr (SX) cn = fminf(cn, readlane_f(cXSF, o >> 1) + CF.y);
+                asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+                             : "+v"(viol)
+                             : "v"(s1.y), "v"(s2.y)
+                             : "vcc");
+                auto push = [&](int s, float a, float bb) {
+                    if constexpr (PATHS == 2) push_le(macc[s], a, bb);
+                    else if constexpr (PATHS == 1) push_lt_eqc(macc[s], a, bb, pmC[s]);
+                };
+                if constexpr (PATHS) last_pm = pmv.x;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    if constexpr (PATHS) push(s, xa2[s], xb2[s]);
+                    v[s] = fminf(xa2[s], xb2[s]);
+                }
+                CF = (f2){cn, s2.y};
+                return;
+            }
             const float kas = readlane_f(cAS, o), kaf = readlane_f(cAF, o);
             const float kxss = readlane_f(cXSS, o), kxff = readlane_f(cXFF, o);
-            float eb[SM], ea[SM];
+            {
+                float eb[SM], ea[SM];
+#pragma unroll
+                for (int s = 0; s < SM; ++s) {
+                    eb[s] = EB[s][o];
+                    ea[s] = EA[s][o];
+                }
+#pragma unroll
+                for (int s = 0; s < SM; ++s) asm volatile("" : "+v"(eb[s]), "+v"(ea[s]));  // one idx block
+                if constexpr (R < 0) chain_terms(xb[0], xa[0], eb[0], ea[0], in.b, CF.y, v[SM - 1]);
+                else chain_terms_v<R>(xb[0], xa[0], eb[0], ea[0], in.b, CF.y, v[SM - 1]);
+#pragma unroll
+                for (int s = 1; s < SM; ++s) {
+                    xa[s] = ea[s] + CF.y;
+                    xb[s] = eb[s] + v[s - 1];
+                }
+            }
+            float vn[SM];
+            auto push = [&](int s, float a, float bb) {  // PATHS: F's term taken (row t-1's bit)
+                if constexpr (PATHS == 2) push_le(macc[s], a, bb);
+                else if constexpr (PATHS == 1) push_lt_eqc(macc[s], a, bb, pmC[s]);
+            };
 #pragma unroll
             for (int s = 0; s < SM; ++s) {
-                eb[s] = EB[s][o];
-                ea[s] = EA[s][o];
-            }
-#pragma unroll
-            for (int s = 0; s < SM; ++s) asm volatile("" : "+v"(eb[s]), "+v"(ea[s]));  // one idx block
-            float vn[SM];
-            auto push = [&](int s, float xa, float xb) {  // PATHS: F's term taken (row t-1's bit)
-                if constexpr (PATHS == 2) push_le(macc[s], xa, xb);
-                else if constexpr (PATHS == 1) push_lt_eqc(macc[s], xa, xb, pmC[s]);
-            };
-            {
-                float xb, xa;
-                chain(xb, xa, eb[0], ea[0], CF.y, v[SM - 1]);
-                vn[0] = fminf(xa, xb);
-                if constexpr (PATHS) push(0, xa, xb);
-            }
-#pragma unroll
-            for (int s = 1; s < SM; ++s) {
-                const float xa = ea[s] + CF.y, xb = eb[s] + v[s - 1];
-                vn[s] = fminf(xa, xb);
-                if constexpr (PATHS) push(s, xa, xb);
+                vn[s] = fminf(xa[s], xb[s]);
+                if constexpr (PATHS) push(s, xa[s], xb[s]);
             }
             // heavy side from the scores of t-1
             float pm = v[0];
@@ -479,9 +604,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 if constexpr (DST == 2) {
                     if ((t & 63u) == 0) wait_cons((int)t - (int)kGR + 64);
                 }
-                step(o, [&](float& xb, float& xa, float eb, float ea, float f, float xl) {
-                    chain_terms(xb, xa, eb, ea, bprev, f, xl);
-                });
+                step(o, ChainIn<-1>{bprev});
                 ring_put(t, v[SM - 1]);
                 if constexpr (DST == 2) put_gran1(t, readlane_f(v[SM - 1], 63));
                 paths_after_rt(t);
@@ -605,13 +728,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             }
                             if constexpr (SRC == 1) bv = bv_next;
                             if constexpr (k == 0) {
-                                step(o, [&](float& xb, float& xa, float eb, float ea, float f, float xl) {
-                                    chain_terms_v<7>(xb, xa, eb, ea, bv_prev, f, xl);
-                                });
+                                step(o, ChainIn<7>{bv_prev});
                             } else {
-                                step(o, [&](float& xb, float& xa, float eb, float ea, float f, float xl) {
-                                    chain_terms_v<(int)k - 1>(xb, xa, eb, ea, bv, f, xl);
-                                });
+                                step(o, ChainIn<(int)k - 1>{bv});
                             }
                             ring_w[(8 * j + k) * 64 + lane] = v[SM - 1];
                             paths_after(tg + k, std::bool_constant<j == 0 && k == 0>{},
@@ -837,6 +956,7 @@ hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratc
         b.nseq > x.rows || x.G < m.G)
         return hipErrorInvalidValue;
     if (paths && (!b.ckpt || !b.prec || !b.fck || !m.pflags)) return hipErrorInvalidValue;
+    if (SVH_PIPE_TAB == 3 && m.SM == 2 && m.S > kT3Sym) return hipErrorInvalidValue;  // mode 3's table size
     if (b.nseq == 0) return hipSuccess;
     PipeModel mm = m;
     FusedBatch bb = b;
