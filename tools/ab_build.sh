@@ -6,6 +6,11 @@ set -e
 cd "$(dirname "$0")/.."
 NAME=$1; FLAGS=$2
 D=build_ab/$NAME
-mkdir -p $D
+mkdir -p $D/obj
+# objects the flags do not change come from the tree's build (make then rebuilds only what differs:
+# pass REBUILD=all to build everything with the flags)
+if [ -z "$REBUILD" ] && [ -d build ]; then
+    for o in build/*.o; do case $o in build/pipe.o) ;; *) cp -p $o $D/obj/ ;; esac; done
+fi
 make -j8 BUILD=$D/obj LIB=$D/libspec_viterbi_hip.so EXTRA_HIPFLAGS="$FLAGS" $D/libspec_viterbi_hip.so > $D/build.log 2>&1
 echo "built $D/libspec_viterbi_hip.so"
