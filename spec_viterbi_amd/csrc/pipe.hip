@@ -65,10 +65,18 @@ static_assert(kGst < 8, "granule store step");
 
 template <uint32_t N>
 __device__ __forceinline__ void wait_vmcnt() {
-    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    static_assert(N < 64, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+
+// The granule consumer's progress store (once per 32 observations, after the prefetch of the last
+// group) is a vector-memory operation too: the next iteration's first two groups have it queued
+// after their own prefetch, so they wait for one operation more than kGpf - 1, or the in-order
+// vmcnt would make them wait for the younger prefetch (issued one group earlier) as well.  A/B knob
+// (SVH_PIPE_VMS=0: the old count).
+#ifndef SVH_PIPE_VMS
+#define SVH_PIPE_VMS 0
+#endif
 
 // One lane's LDS store of a wave-uniform word: EXEC narrowed to lane 0 inside the asm (no
 // divergent branch in the compiler's view).
@@ -656,9 +664,16 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             // body: 32 observations per iteration, four groups of 8
             if (t + 32 <= len) {
                 uint64_t gq[kGpf] = {};  // SRC 2: granule groups in flight
+                // SRC 2 waves whose only body stores are the progress words (see SVH_PIPE_VMS)
+                constexpr bool kVmStore = SVH_PIPE_VMS && SRC == 2 && DST != 2 && PATHS == 0 && kGpf == 2;
                 if constexpr (SRC == 2) {
 #pragma unroll
                     for (uint32_t j = 0; j < kGpf; ++j) g_prefetch64(gq[j], gin + ((t + 8 * j + (lane & 7u)) & (kGR - 1)));
+                    // store-aware counts: the first iteration's first two groups also find one store
+                    // queued behind their prefetches (the progress word again: observations < t done)
+                    if constexpr (kVmStore) {
+                        if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | t);
+                    }
                 }
                 float gpend = 0.0f;    // DST 2: the previous group's boundary scores (lanes 0..7),
                 uint32_t gpend_t = 0;  // read back from the ring one group before they are stored
@@ -702,7 +717,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         const uint32_t tg = t + 8 * j;
                         float bv = kInf;  // lanes 0..7: the previous block's last scores of tg..tg+7
                         if constexpr (SRC == 2) {
-                            wait_vmcnt<kGpf - 1>();  // gq[j]: kGpf - 1 later loads in flight
+                            // gq[j]: kGpf - 1 later loads in flight (+ the progress store, groups 0, 1)
+                            if constexpr (kVmStore && j < 2) wait_vmcnt<kGpf>();
+                            else wait_vmcnt<kGpf - 1>();
                             uint64_t gv = gq[j % kGpf];
                             while (__builtin_amdgcn_ballot_w64((uint32_t)(gv >> 32) != gtag(ep, tg)) != 0) {
                                 if (dbg) ++dg[5];
