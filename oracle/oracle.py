@@ -36,6 +36,7 @@ def _load():
     lib.ora_argmin.restype = ctypes.c_int64
     lib.ora_viterbi_spec.argtypes = [P, ctypes.c_uint32, _u64, ctypes.c_uint64, _f32]
     lib.ora_spec_products.argtypes = [P, ctypes.c_uint32, _f32]
+    lib.ora_viterbi_spec_batch.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64, _u64, _u64, _f32]
     lib.ora_viterbi_batch.argtypes = [P, ctypes.c_uint64, _u64, _u64, _f32, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_int)]
     return lib
@@ -93,6 +94,19 @@ def viterbi_spec(hmm, level: int, seq):
     out = np.empty(m.n, np.float32)
     _rc(lib.ora_viterbi_spec(ctypes.byref(m.s), int(level), seq.ctypes.data_as(_u64), seq.size,
                              out.ctypes.data_as(_f32)))
+    return out
+
+
+def viterbi_spec_batch(hmm, level: int, seqs):
+    """viterbi_spec over many sequences with the products built once: scores [nseq, n]."""
+    m = _Model(hmm)
+    seqs = [np.ascontiguousarray(s, np.uint64) for s in seqs]
+    offsets = np.zeros(len(seqs) + 1, np.uint64)
+    offsets[1:] = np.cumsum([s.size for s in seqs])
+    symbols = np.ascontiguousarray(np.concatenate(seqs), np.uint64)
+    out = np.empty((len(seqs), m.n), np.float32)
+    _rc(lib.ora_viterbi_spec_batch(ctypes.byref(m.s), int(level), len(seqs), offsets.ctypes.data_as(_u64),
+                                   symbols.ctypes.data_as(_u64), out.ctypes.data_as(_f32)))
     return out
 
 

@@ -364,3 +364,85 @@ done:
     csr_free(&c);
     return rc;
 }
+
+/* Spec Viterbi of many sequences with one set of products (the same arithmetic as
+ * ora_viterbi_spec, GraphBLAS_spec_impl.cpp:50-89, with spec_with's precompute :146-181 done once
+ * as the reference's object does): OpenMP over sequences, each chunk product serial. */
+int ora_viterbi_spec_batch(const ora_hmm* h, uint32_t level, uint64_t nseq, const uint64_t* offsets,
+                           const uint64_t* symbols, float* out) {
+    if (!h || !offsets || !out || h->n == 0) return ORA_EINVAL;
+    for (uint64_t q = 0; q < nseq; ++q) {
+        int rc = check_seq(h, symbols + offsets[q], offsets[q + 1] - offsets[q]);
+        if (rc) return rc;
+    }
+    ora_csr c;
+    int rc = csr_build(h, &c);
+    if (rc) return rc;
+    const uint64_t n = h->n;
+    float* start = (float*)malloc(n * sizeof(float));
+    float* prod = NULL;
+    if (!start) {
+        rc = ORA_ENOMEM;
+        goto done;
+    }
+    rc = start_build(h, start);
+    if (rc) goto done;
+    if (level > 1) {
+        prod = (float*)malloc(ipow(h->S, level) * n * n * sizeof(float));
+        if (!prod) {
+            rc = ORA_ENOMEM;
+            goto done;
+        }
+        rc = ora_spec_products(h, level, prod);
+        if (rc) goto done;
+    }
+    int fail = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : fail)
+    for (int64_t q = 0; q < (int64_t)nseq; ++q) {
+        const uint64_t* seq = symbols + offsets[q];
+        const uint64_t len = offsets[q + 1] - offsets[q];
+        float* a = (float*)malloc(n * sizeof(float));
+        float* b = (float*)malloc(n * sizeof(float));
+        if (!a || !b) {
+            free(a);
+            free(b);
+            fail |= 1;
+            continue;
+        }
+        first_step(h, start, seq[0], a);
+        uint64_t i = 1;
+        if (level > 1) {
+            while (len - i >= level) {
+                uint64_t key = 0;
+                for (uint32_t k = 0; k < level; ++k, ++i) key = key * h->S + seq[i];
+                const float* H = prod + key * n * n;
+                for (uint64_t j = 0; j < n; ++j) {
+                    float best = INFINITY;
+                    for (uint64_t m = 0; m < n; ++m) {
+                        const float t = H[j * n + m] + a[m];
+                        if (t < best) best = t;
+                    }
+                    b[j] = best;
+                }
+                float* t = a;
+                a = b;
+                b = t;
+            }
+        }
+        for (; i < len; ++i) {
+            step(h, &c, seq[i], a, b, NULL);
+            float* t = a;
+            a = b;
+            b = t;
+        }
+        memcpy(out + (uint64_t)q * n, a, n * sizeof(float));
+        free(a);
+        free(b);
+    }
+    if (fail) rc = ORA_ENOMEM;
+done:
+    free(prod);
+    free(start);
+    csr_free(&c);
+    return rc;
+}

@@ -71,6 +71,10 @@ int ora_viterbi_spec(const ora_hmm* h, uint32_t level, const uint64_t* seq, uint
  * first observed symbol most significant: out[(key * n + j) * n + m].  Size S^L * n * n. */
 int ora_spec_products(const ora_hmm* h, uint32_t level, float* out);
 
+/* Spec Viterbi of many sequences sharing one set of level-L products: out[nseq * n]. */
+int ora_viterbi_spec_batch(const ora_hmm* h, uint32_t level, uint64_t nseq, const uint64_t* offsets,
+                           const uint64_t* symbols, float* out);
+
 /* Batch of sequences (CPU baseline): offsets[nseq+1] into symbols; out[nseq * n].
  * nthreads <= 0 means "all available". Returns threads actually used via *used (nullable). */
 int ora_viterbi_batch(const ora_hmm* h, uint64_t nseq, const uint64_t* offsets,

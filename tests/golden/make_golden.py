@@ -6,6 +6,7 @@ Floats are stored as IEEE-754 bit patterns (hex) so the vectors are exact.
 
     python tests/golden/make_golden.py            # the fixture files below
     python tests/golden/make_golden.py digests    # score_digests.json (bench workloads)
+    python tests/golden/make_golden.py spec2      # + level-2 digests of every emit_50 row (config 4)
 """
 from __future__ import annotations
 
@@ -68,13 +69,48 @@ def digests():
                          "path_sha256": hashlib.sha256(np.asarray(path, np.int32).tobytes()).hexdigest()})
         out[f"2405.chmm x {ess}"] = rows
         print("digests", ess, len(rows))
-    with open(os.path.join(OUT, "score_digests.json"), "w") as f:
+    path = os.path.join(OUT, "score_digests.json")
+    if os.path.exists(path):  # keep the level-2 rows (spec2_digests) in the same file
+        with open(path) as f:
+            out = {**json.load(f), **out}
+    with open(path, "w") as f:
         json.dump(out, f, indent=0)
+
+
+SPEC2_KEY = "2405.chmm x emit_50_3500_20.ess level 2"
+
+
+def spec2_digests():
+    """Level-2 (_spec) score digests of all 50 rows of 2405.chmm x emit_50_3500_20 (BASELINE
+    config 4): the oracle builds the 400 dense products once (9.3 GB) and runs every row with them
+    (GraphBLAS_spec_impl.cpp:50-89, 146-181).  Added to score_digests.json under SPEC2_KEY; rows 0..1
+    are cross-checked against the full vectors in chmm2405_emit50.json first."""
+    import hashlib
+
+    hmm = svh.read_HMM(os.path.join(DATA, "chmm_files/2405.chmm"))
+    seqs = svh.read_emit_seq(os.path.join(DATA, "ess_files/emit_50_3500_20.ess"))
+    scores = oracle.viterbi_spec_batch(hmm, 2, seqs)
+    with open(os.path.join(OUT, "chmm2405_emit50.json")) as f:
+        g = json.load(f)
+    for rec in g["sequences"]:
+        assert hexbits(scores[rec["index"]]) == rec["spec"]["2"], rec["index"]
+    rows = [{"length": int(s.size), "scores_sha256": hashlib.sha256(np.asarray(r, np.float32).tobytes()).hexdigest()}
+            for s, r in zip(seqs, scores)]
+    path = os.path.join(OUT, "score_digests.json")
+    with open(path) as f:
+        out = json.load(f)
+    out[SPEC2_KEY] = rows
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0)
+    print("spec2 digests", len(rows))
 
 
 def main():
     if sys.argv[1:] == ["digests"]:
         digests()
+        return
+    if sys.argv[1:] == ["spec2"]:
+        spec2_digests()
         return
     goldens = {
         "test_chmms": [case(f"chmm_files/test_chmms/{i}_test_chmm.chmm", f"ess_files/test_sequences/{i}_test_seq.ess",

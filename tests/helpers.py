@@ -16,6 +16,12 @@ def load_golden(name):
         return json.load(f)
 
 
+def load_digests():
+    """tests/golden/score_digests.json: per-row SHA-256 of the oracle's float32 scores (+ paths)."""
+    with open(os.path.join(GOLDEN, "score_digests.json")) as f:
+        return json.load(f)
+
+
 def from_hex(bits):
     return np.array([struct.unpack("<f", bytes.fromhex(b))[0] for b in bits], np.float32)
 

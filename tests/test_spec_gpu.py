@@ -6,7 +6,7 @@ import spec_viterbi_amd as svh
 from spec_viterbi_amd import _lib
 from oracle import oracle
 from tests.conftest import chmm, ess
-from tests.helpers import bit_equal, first_mismatch, from_hex, load_golden, random_hmm, random_seqs
+from tests.helpers import bit_equal, first_mismatch, from_hex, load_digests, load_golden, random_hmm, random_seqs
 
 pytestmark = pytest.mark.gpu
 
@@ -63,9 +63,12 @@ def test_spec_level2_500_model():
 def test_spec_level2_2405_emit50_config4():
     """BASELINE config 4: 2405.chmm x emit_50_3500_20.ess on the _spec level-2 path (400 dense
     2407 x 2408 products, 9.3 GB of HBM; reference GraphBLAS_spec_impl.cpp:15-36, :68-80).
-    All 50 sequences run in one batch; sequences 0..1 are compared bit-exact against the oracle's
-    committed level-2 vectors, every sequence against the non-spec goldens' tolerance rule
-    (HMM::almost_equal, |diff| <= 1, the reference's own semantic-equality bound)."""
+    All 50 sequences run in one batch and every row is compared bit-exact against the oracle's
+    level-2 scores: rows 0..1 against the committed vectors, all 50 against the SHA-256 digests of
+    the oracle's float32 rows (tests/golden/make_golden.py spec2); every row also within the
+    reference's semantic-equality bound (HMM::almost_equal, |diff| <= 1) of the non-spec scores."""
+    import hashlib
+
     g = load_golden("chmm2405_emit50")
     hmm = svh.read_HMM(chmm("2405.chmm"))
     seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
@@ -76,6 +79,11 @@ def test_spec_level2_2405_emit50_config4():
     for rec in g["sequences"]:
         ref = from_hex(rec["spec"]["2"])
         assert bit_equal(got[rec["index"]], ref), (rec["index"], first_mismatch(got[rec["index"]], ref))
+    rows = load_digests()["2405.chmm x emit_50_3500_20.ess level 2"]
+    assert len(rows) == 50
+    bad = [q for q in range(50)
+           if hashlib.sha256(np.ascontiguousarray(got[q], np.float32).tobytes()).hexdigest() != rows[q]["scores_sha256"]]
+    assert not bad, f"level-2 rows differing from the oracle digests: {bad}"
     nonspec = svh.DeviceModel(hmm).viterbi(seqs)[0]
     assert np.all(np.abs(got - nonspec) <= 1.0)
     assert not np.array_equal(got, nonspec)  # level 2 really took the product path
