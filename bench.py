@@ -207,7 +207,7 @@ def cpu_baseline(hmm, seqs, seconds: float) -> dict:
 # ---- rocprofv3 PMC passes (children on tools/launch.py) ---------------------------------------
 PMC_PASSES = {
     "sq": ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
-           "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE"],
+           "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE"],
     "fetch": ["FETCH_SIZE"],
     "write": ["WRITE_SIZE"],
 }
@@ -250,7 +250,16 @@ def pmc_counters(launch_args: list[str], kernel_prefix: str) -> dict | None:
     return out or None
 
 
-def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc) -> dict:
+def essential_bytes_per_launch(n: int, S: int, lengths, paths: bool) -> int:
+    """HBM bytes a launch cannot avoid: the symbols (uint8) in, the scores (fp32) and best states
+    (int64) out, the model's folded (eb, ea) tables (S x n float pairs) read once, and with paths
+    the decoded path (int32 per observation).  SURVEY 8(d)'s streamed-CSR bytes are not this
+    kernel's bound (it keeps the model and the scores on chip): reported as bytes only."""
+    nseq = len(lengths)
+    return sum(lengths) + nseq * n * 4 + nseq * 8 + S * n * 8 + (4 * sum(lengths) if paths else 0)
+
+
+def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc, essential_bytes) -> dict:
     """VALU-issue roofline of the step kernels (the per-observation step is VALU + LDS work on
     registers; HBM carries only symbols in and scores out).  Capacity of one SIMD-32: one wave64
     VALU instruction per 2 cycles, and at most one per 4 cycles from a single wave
@@ -279,10 +288,11 @@ def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc) -> dict:
            "achieved": None, "frac": None, "traffic": None, "kernel_ms": round(kernel_ms, 4),
            "occupancy": {"cus": cus, "of_cus": info["cu_count"], "waves_per_simd": waves_per_simd,
                          "workgroups_per_cu": wg_per_cu}}
-    gbs = algo_bytes / (kernel_ms * 1e-3) / 1e9
-    res["hbm"] = {"algorithmic_bytes": int(algo_bytes), "algorithmic_GBps": round(gbs, 1),
-                  "algorithmic_frac": round(gbs / HBM_PEAK_GBS, 4), "peak_GBps": HBM_PEAK_GBS,
-                  "measured_bytes": None, "measured_GBps": None, "measured_frac": None}
+    egbs = essential_bytes / (kernel_ms * 1e-3) / 1e9
+    res["hbm"] = {"essential_bytes": int(essential_bytes), "essential_GBps": round(egbs, 2),
+                  "essential_frac": round(egbs / HBM_PEAK_GBS, 6), "peak_GBps": HBM_PEAK_GBS,
+                  "measured_bytes": None, "measured_GBps": None, "measured_frac": None,
+                  "measured_over_essential": None, "streamed_csr_model_bytes": int(algo_bytes)}
     peak_chip = info["cu_count"] * 4 * 0.5 * CLOCK_GHZ if info["cu_count"] else 256 * 4 * 0.5 * CLOCK_GHZ
     res["peak_chip"] = round(peak_chip, 2)
     res["frac_chip"] = None
@@ -303,6 +313,12 @@ def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc) -> dict:
         if "SQ_WAVE_CYCLES" in pmc and "SQ_WAVES" in pmc:  # quad-cycles
             res["wave_cycles"] = round(4 * pmc["SQ_WAVE_CYCLES"] / pmc["SQ_WAVES"], 0)
             res["wait_frac"] = round(pmc.get("SQ_WAIT_ANY", 0) / pmc["SQ_WAVE_CYCLES"], 4)
+            # the three disjoint shares of a wave's cycles (MI355X_MICROARCH.md, PMC slots): issuing,
+            # issue stalls (dependencies / pipe busy), parked on s_waitcnt / s_sleep / barriers
+            if "SQ_ACTIVE_INST_ANY" in pmc and "SQ_WAIT_INST_ANY" in pmc:
+                res["cycle_split"] = {k: round(pmc.get(c, 0) / pmc["SQ_WAVE_CYCLES"], 4) for k, c in
+                                      (("active_inst", "SQ_ACTIVE_INST_ANY"), ("wait_inst", "SQ_WAIT_INST_ANY"),
+                                       ("wait_any", "SQ_WAIT_ANY"))}
         if "GRBM_GUI_ACTIVE" in pmc:
             res["profiled_clock_ghz"] = round(pmc["GRBM_GUI_ACTIVE"] / 8 / (kernel_ms * 1e6), 3)
     if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:  # KiB; FETCH_SIZE doubled on gfx950
@@ -310,14 +326,16 @@ def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc) -> dict:
         res["traffic"] = round(traffic)
         mg = traffic / (kernel_ms * 1e-3) / 1e9
         res["hbm"].update(measured_bytes=round(traffic), measured_GBps=round(mg, 2),
-                          measured_frac=round(mg / HBM_PEAK_GBS, 6))
+                          measured_frac=round(mg / HBM_PEAK_GBS, 6),
+                          measured_over_essential=round(traffic / max(essential_bytes, 1), 2))
     res["note"] = ("frac = VALU wave-instructions issued (rocprofv3 SQ_INSTS_VALU, child pass on tools/launch.py) / "
                    "kernel time, over the issue capacity of the SIMDs the launch occupies at its occupancy, at 2.4 GHz; "
                    "frac_chip = the same over the whole chip (CUs x 4 SIMDs x 1/2 per cycle x 2.4 GHz); issue_frac_all = "
                    "VALU + SALU + LDS instructions over one wave's issue rate (1 per 4 cycles) on the occupied SIMDs; "
-                   "hbm.algorithmic_* "
-                   "is SURVEY 8(d)'s streamed-CSR model (47.98 B/state-update; the kernel keeps the model on chip, so it "
-                   "is not a bound), hbm.measured_* the PMC bytes (FETCH_SIZE x2 + WRITE_SIZE)")
+                   "hbm.essential_* = the bytes a launch cannot avoid (symbols in, scores and best states out, the "
+                   "folded tables once); hbm.measured_* the PMC bytes (FETCH_SIZE x2 + WRITE_SIZE) and their ratio to "
+                   "the essential bytes; hbm.streamed_csr_model_bytes = SURVEY 8(d)'s streamed-CSR model (47.98 "
+                   "B/state-update), not a bound for a kernel that keeps the model on chip, so no rate is derived from it")
     return res
 
 
@@ -509,7 +527,9 @@ def main(argv=None):
                      "--warmup", "1"]
             kpref = {4: "chain_viterbi_kernel", 5: "pipe_viterbi_kernel", 6: "pipew_viterbi_kernel"}[plan["kernel"]]
             pmc = pmc_counters(largs, "void svh::(anonymous namespace)::" + kpref)
-        rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc)
+        # level >= 2 streams one dense product per chunk from HBM: those bytes are its bound
+        ess_b = algo if args.level >= 2 else essential_bytes_per_launch(n, int(info["S"]), lengths, args.paths)
+        rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc, ess_b)
         workload = (f"{args.model} x {ess_name}" +
                     (f" x{args.replicate} (file sequences + same-shape synthetic copies)" if args.replicate > 1 else "") +
                     (", LPT-sharded (strong scaling)" if strong else "") + ", " +

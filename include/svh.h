@@ -215,6 +215,15 @@ int svh_decode_file(svh_model_t m, const char* path, int format, uint32_t level,
  * model are serialised. */
 int svh_viterbi(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* offsets,
                 const uint64_t* symbols, float* scores, int64_t* best_state, int32_t* paths);
+/* The same from packed uint8 symbols (the device format: e.g. svh_reader_next's output), */
+int svh_viterbi_u8(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* offsets,
+                   const uint8_t* symbols, float* scores, int64_t* best_state, int32_t* paths);
+/* ... and from nseq separate symbol arrays (seqs[q], lens[q] symbols each: the reference's
+ * HMM::Emit_seq_vec_t, a vector of vectors, or a list of arrays) without the caller flattening
+ * them: each is narrowed straight into the pinned upload.  Paths (when requested) are written
+ * back to back in sequence order. */
+int svh_viterbi_seqs(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* const* seqs,
+                     const uint64_t* lens, float* scores, int64_t* best_state, int32_t* paths);
 
 #ifdef __cplusplus
 }

@@ -92,6 +92,8 @@ SIGNATURES = {
     "svh_batch_debug_fault": (c_int, [c_void_p, c_void_p]),
     "svh_batch_destroy": (c_int, [c_void_p]),
     "svh_viterbi": (c_int, [c_void_p, c_uint32, c_uint64, P_u64, P_u64, P_f32, P_i64, P_i32]),
+    "svh_viterbi_u8": (c_int, [c_void_p, c_uint32, c_uint64, P_u64, POINTER(ctypes.c_uint8), P_f32, P_i64, P_i32]),
+    "svh_viterbi_seqs": (c_int, [c_void_p, c_uint32, c_uint64, P_u64, P_u64, P_f32, P_i64, P_i32]),
     "svh_batch_create_u8": (c_int, [c_void_p, c_uint64, P_u64, POINTER(ctypes.c_uint8), c_uint32, POINTER(c_void_p)]),
     "svh_batch_run_time_parallel": (c_int, [c_void_p, c_uint32, c_uint32, c_float, c_void_p, P_u64]),
     "svh_reader_open": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),

@@ -63,6 +63,17 @@ constexpr uint32_t kGst = SVH_PIPE_GST;
 static_assert(kGpf == 1 || kGpf == 2 || kGpf == 4, "granule prefetch depth");
 static_assert(kGst < 8, "granule store step");
 
+// LDS boundary ring layout (A/B knob): 0 = [u][lane] (every step stores its row, one ds_write_b32);
+// 1 = [u / 8][lane][u % 8]: a group's 8 last-slot scores stay in registers and go out as two
+// ds_write_b128 per group (the consumer reads lane 63's 8 values as one contiguous 32 bytes).
+#ifndef SVH_PIPE_RING8
+#define SVH_PIPE_RING8 0
+#endif
+// ring slot of cycle position u (0..31) and lane l
+__device__ __forceinline__ uint32_t ring_idx(uint32_t u, uint32_t l) {
+    return SVH_PIPE_RING8 ? ((u >> 3) * 64 + l) * 8 + (u & 7u) : u * 64 + l;
+}
+
 template <uint32_t N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N < 64, "vmcnt");
@@ -143,7 +154,7 @@ __device__ __forceinline__ void chain_terms_v(float& xb, float& xa, float eb, fl
 #ifndef SVH_PIPE_TAB
 #define SVH_PIPE_TAB 0
 #endif
-static_assert(SVH_PIPE_TAB == 0 || SVH_PIPE_TAB == 3, "table read mode");
+static_assert(SVH_PIPE_TAB == 0 || SVH_PIPE_TAB == 3 || SVH_PIPE_TAB == 4, "table read mode");
 
 // Slot 0's chain input for a step: R < 0 the uniform boundary b (SGPR, single observations),
 // R = 0 lane 0 of the group vector, R = 1..7 lane R of the group vector (row_ror:16-R).
@@ -267,7 +278,8 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 EA[s][o] = (uint32_t)o < S ? e.y : kInf;
             }
         // mode 3: the pair-interleaved tables (symbols >= S: +inf)
-        constexpr bool kT3 = SVH_PIPE_TAB == 3 && SM == 2;
+        constexpr bool kT3 = (SVH_PIPE_TAB == 3 || SVH_PIPE_TAB == 4) && SM == 2;  // pair tables
+        constexpr bool kT4 = SVH_PIPE_TAB == 4 && SM == 2;  // ... read by four 64-bit moves
         f32x32 TA[4];
         f32x8 TB[4];
         if constexpr (kT3) {
@@ -289,6 +301,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         else TB[k][r - 32] = val[k][u];
                     }
             }
+            // opaque per-lane values: the heavy constants are wave-uniform, and the compiler would
+            // otherwise keep them in SGPRs and copy them into the pinned registers at every step
+#pragma unroll
+            for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(TA[k]), "+v"(TB[k]));
         }
         // heavy constants as lane tables (lane o: symbol o), extracted with v_readlane
         const bool lo = lane < S;
@@ -454,7 +470,44 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         auto step = [&](uint32_t o, auto in) {
             constexpr int R = decltype(in)::value;
             float xa[SM], xb[SM];  // feeder and chain terms of every slot
-            if constexpr (kT3) {  // o is 2 x the symbol
+            if constexpr (kT4) {  // o is 2 x the symbol: four 64-bit moves out of the pair tables
+                f2 p0, p1, kS, kX;  // {eb_0, ea_0}, {eb_1, ea_1}, {A_S, A_F}, {X_SS, X_FF}
+                asm("s_set_gpr_idx_on %[o], gpr_idx(SRC0)\n\t"
+                    "v_mov_b64 %[p0], v[2:3]\n\t"
+                    "v_mov_b64 %[p1], v[42:43]\n\t"
+                    "v_mov_b64 %[ks], v[82:83]\n\t"
+                    "v_mov_b64 %[kx], v[122:123]\n\t"
+                    "s_set_gpr_idx_off"
+                    : [p0] "=&v"(p0), [p1] "=&v"(p1), [ks] "=&v"(kS), [kx] "=&v"(kX)
+                    : [o] "s"(o), "{v[2:33]}"(TA[0]), "{v[34:41]}"(TB[0]), "{v[42:73]}"(TA[1]), "{v[74:81]}"(TB[1]),
+                      "{v[82:113]}"(TA[2]), "{v[114:121]}"(TB[2]), "{v[122:153]}"(TA[3]), "{v[154:161]}"(TB[3])
+                    : "m0");
+                if constexpr (R < 0) chain_terms(xb[0], xa[0], p0.x, p0.y, in.b, CF.y, v[1]);
+                else chain_terms_v<R>(xb[0], xa[0], p0.x, p0.y, in.b, CF.y, v[1]);
+                xa[1] = p1.y + CF.y;
+                xb[1] = p1.x + v[0];
+                const float pm = fminf(v[0], v[1]);
+                const f2 s1 = kS + (f2){pm, pm};  // A_S + m, A_F + m
+                const f2 s2 = kX + CF;            // X_SS + c, X_FF + F
+                float cn = fminf(s1.x, s2.x);
+                if constexpr (SX) cn = fminf(cn, readlane_f(cXSF, o >> 1) + CF.y);
+                asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+                             : "+v"(viol)
+                             : "v"(s1.y), "v"(s2.y)
+                             : "vcc");
+                auto push = [&](int s, float a, float bb) {
+                    if constexpr (PATHS == 2) push_le(macc[s], a, bb);
+                    else if constexpr (PATHS == 1) push_lt_eqc(macc[s], a, bb, pmC[s]);
+                };
+                if constexpr (PATHS) last_pm = pm;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    if constexpr (PATHS) push(s, xa[s], xb[s]);
+                    v[s] = fminf(xa[s], xb[s]);
+                }
+                CF = (f2){cn, s2.y};
+                return;
+            } else if constexpr (kT3) {  // o is 2 x the symbol
                 float vv[2] = {v[0], v[SM - 1]};
                 float xa2[2], xb2[2];
                 f2 pmv;
@@ -599,7 +652,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             const uint64_t gv = ((uint64_t)gtag(ep, s) << 32) | __builtin_bit_cast(uint32_t, val);
             if (lane == 0) g_st64(gout + (s & (kGR - 1)), gv);
         };
-        auto ring_put = [&](uint32_t t, float val) { ring_w[((t - tb) & (kR - 1)) * 64 + lane] = val; };
+        auto ring_put = [&](uint32_t t, float val) { ring_w[ring_idx((t - tb) & (kR - 1), lane)] = val; };
 
         // The sweep, with the boundary roles as compile-time constants (one code path per role).
         auto sweep = [&](auto srcc, auto dstc) {
@@ -620,7 +673,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                     if constexpr (SRC == 1) {
                         wait_prev(t + 1);
                         asm volatile("" ::: "memory");
-                        bprev = readlane_f(ring_prev[((t - tb) & (kR - 1)) * 64 + 63], 0);
+                        bprev = readlane_f(ring_prev[ring_idx((t - tb) & (kR - 1), 63)], 0);
                     } else if constexpr (SRC == 2) {
                         bprev = gran_single(t);
                     }
@@ -640,7 +693,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             if constexpr (SRC == 1) {
                 wait_prev(first);
                 asm volatile("" ::: "memory");
-                bprev = readlane_f(ring_prev[((first - 1 - tb) & (kR - 1)) * 64 + 63], 0);
+                bprev = readlane_f(ring_prev[ring_idx((first - 1 - tb) & (kR - 1), 63)], 0);
             } else if constexpr (SRC == 2) {
                 // initial progress (observations < first are done), published before the first
                 // poll: a row that starts mid-sequence at a multiple of 64 would otherwise leave its
@@ -690,7 +743,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 // next_ok) into this one loop-carried register, re-loaded there when it was stale
                 float bv_next = kInf;
                 bool next_ok = false;
-                if constexpr (SRC == 1) bv_next = ring_prev[(lane & 7u) * 64 + 63];  // group at t (u % 32 == 0)
+                if constexpr (SRC == 1) bv_next = ring_prev[ring_idx(lane & 7u, 63)];  // group at t (u % 32 == 0)
                 while (t + 32 <= len) {
                   // the window of t, loaded and waited for here (an asm use), so no load of it is
                   // pending inside the iterations: the compiler would otherwise wait for every
@@ -716,6 +769,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         constexpr uint32_t j = decltype(jc)::value;
                         const uint32_t tg = t + 8 * j;
                         float bv = kInf;  // lanes 0..7: the previous block's last scores of tg..tg+7
+                        float gl[8];      // SVH_PIPE_RING8: this group's last-slot scores
                         if constexpr (SRC == 2) {
                             // gq[j]: kGpf - 1 later loads in flight (+ the progress store, groups 0, 1)
                             if constexpr (kVmStore && j < 2) wait_vmcnt<kGpf>();
@@ -740,7 +794,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                 if (!next_ok) {  // the producer had not published this group: wait, re-load
                                     wait_prev(tg + 8);
                                     asm volatile("" ::: "memory");
-                                    bv_next = ring_prev[(8 * j + (lane & 7u)) * 64 + 63];
+                                    bv_next = ring_prev[ring_idx(8 * j + (lane & 7u), 63)];
                                 }
                             }
                             if constexpr (SRC == 1) bv = bv_next;
@@ -749,7 +803,14 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             } else {
                                 step(o, ChainIn<(int)k - 1>{bv});
                             }
-                            ring_w[(8 * j + k) * 64 + lane] = v[SM - 1];
+                            if constexpr (SVH_PIPE_RING8) {  // kept for the group's two 16-byte stores
+                                gl[k] = v[SM - 1];
+                                if constexpr (k == 3 || k == 7)
+                                    *reinterpret_cast<float4*>(ring_w + ring_idx(8 * j + k - 3, lane)) =
+                                        make_float4(gl[k - 3], gl[k - 2], gl[k - 1], gl[k]);
+                            } else {
+                                ring_w[ring_idx(8 * j + k, lane)] = v[SM - 1];
+                            }
                             paths_after(tg + k, std::bool_constant<j == 0 && k == 0>{},
                                         std::bool_constant<k == 0 && (j == 0 || j == 2)>{},
                                         std::bool_constant<j == 3 && k == 7>{});
@@ -779,7 +840,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         if constexpr (SRC == 1) {  // the next group's boundary vector (valid if next_ok)
                             next_ok = (uint32_t)uniform((int)pc_rd) >= tg + 16;
                             asm volatile("" ::: "memory");
-                            bv_next = ring_prev[(((8 * j + 8) & (kR - 1)) + (lane & 7u)) * 64 + 63];
+                            bv_next = ring_prev[ring_idx(((8 * j + 8) & (kR - 1)) + (lane & 7u), 63)];
                         }
                         if constexpr (DST == 2) {
                             // granules of the previous group (read back from the ring one group ago)
@@ -788,7 +849,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                     g_st64(gout + ((gpend_t + lane) & (kGR - 1)),
                                            ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
                             }
-                            gpend = ring_w[(8 * j + (lane & 7u)) * 64 + 63];
+                            gpend = ring_w[ring_idx(8 * j + (lane & 7u), 63)];
                             gpend_t = tg;
                         }
                         if constexpr (SRC == 2 && j == 3) {
@@ -945,6 +1006,9 @@ const void* pipe_ptr(bool sx) {
 }
 
 const void* pipe_fn(int sm, int waves, bool sx) {
+#ifdef SVH_PIPE_AB_ONLY  // A/B timing builds: the headline geometry only (compile time)
+    return sm == 2 && waves == 4 && !sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0>) : nullptr;
+#else
     switch (sm * 100 + waves) {
         case 104: return pipe_ptr<1, 4>(sx);
         case 108: return pipe_ptr<1, 8>(sx);
@@ -952,12 +1016,17 @@ const void* pipe_fn(int sm, int waves, bool sx) {
         case 208: return pipe_ptr<2, 8>(sx);
         default: return nullptr;
     }
+#endif
 }
 
 // decoded-path variant: the default geometry only (2 slots, 4 waves)
 const void* pipe_paths_fn(int sm, int waves, bool sx, bool ties_heavy) {
+#ifdef SVH_PIPE_AB_ONLY
+    return nullptr;
+#else
     if (sm != 2 || waves != 4) return nullptr;
     return ties_heavy ? pipe_ptr<2, 4, 2>(sx) : pipe_ptr<2, 4, 1>(sx);
+#endif
 }
 
 }  // namespace
@@ -973,7 +1042,7 @@ hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratc
         b.nseq > x.rows || x.G < m.G)
         return hipErrorInvalidValue;
     if (paths && (!b.ckpt || !b.prec || !b.fck || !m.pflags)) return hipErrorInvalidValue;
-    if (SVH_PIPE_TAB == 3 && m.SM == 2 && m.S > kT3Sym) return hipErrorInvalidValue;  // mode 3's table size
+    if (SVH_PIPE_TAB >= 3 && m.SM == 2 && m.S > kT3Sym) return hipErrorInvalidValue;  // pair tables' size
     if (b.nseq == 0) return hipSuccess;
     PipeModel mm = m;
     FusedBatch bb = b;

@@ -1218,10 +1218,13 @@ void Batch::init(uint32_t flags) {
 // buffers that only ever grow (no hipFree / hipMalloc, hence no device-wide sync, once sized).
 // The host staging arrays are members, so they outlive the copies until the next load.
 void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, const uint8_t* sym8,
-                 hipStream_t s) {
+                 hipStream_t s, const uint64_t* const* seqp) {
     if (nseq_ == 0) throw Error(SVH_E_INVALID, "empty batch");
     if (nseq_ > 0x7FFFFFFFull) throw Error(SVH_E_UNSUPPORTED, "too many sequences in one batch");
-    if (!offs || (!sym64 && !sym8)) throw Error(SVH_E_INVALID, "null offsets/symbols");
+    if (!offs || (!sym64 && !sym8 && !seqp)) throw Error(SVH_E_INVALID, "null offsets/symbols");
+    if (seqp)
+        for (uint64_t q = 0; q < nseq_; ++q)
+            if (!seqp[q] && offs[q + 1] > offs[q]) throw Error(SVH_E_INVALID, "null sequence pointer");
     const DeviceBandPlan* cpl = chain_paths ? model->band_for(true) : nullptr;
     nseq = (uint32_t)nseq_;
     const DevicePipePlan* ppl = chain_paths ? model->pipe_paths_for(nseq) : nullptr;
@@ -1303,26 +1306,34 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
         uint8_t* dstp = hin + s_sym.off + h_symoff[q];
         const uint32_t L = lens[q];
         const uint64_t base = offs[q];
-        if (sym64) {
+        // narrow into pinned staging; the range check is a branch-free OR the loop vectorises,
+        // the error path re-scans for the offending symbol
+        if (sym64 || seqp) {
+            const uint64_t* src = seqp ? seqp[q] : sym64 + base;
             uint64_t bad = 0;
             for (uint32_t i = 0; i < L; ++i) {
-                const uint64_t x = sym64[base + i];
+                const uint64_t x = src[i];
                 bad |= x >= S ? 1u : 0u;
                 dstp[i] = (uint8_t)x;
             }
             if (bad)
                 for (uint32_t i = 0; i < L; ++i)
-                    if (sym64[base + i] >= S)
-                        throw Error(SVH_E_RANGE, "symbol " + std::to_string(sym64[base + i]) +
+                    if (src[i] >= S)
+                        throw Error(SVH_E_RANGE, "symbol " + std::to_string(src[i]) +
                                                      " out of range (emit_num " + std::to_string(S) + ")");
         } else {
+            const uint8_t* src = sym8 + base;
+            uint32_t bad = 0;
             for (uint32_t i = 0; i < L; ++i) {
-                const uint64_t x = sym8[base + i];
-                if (x >= S)
-                    throw Error(SVH_E_RANGE, "symbol " + std::to_string(x) + " out of range (emit_num " +
-                                                 std::to_string(S) + ")");
+                const uint32_t x = src[i];
+                bad |= x >= S ? 1u : 0u;
                 dstp[i] = (uint8_t)x;
             }
+            if (bad)
+                for (uint32_t i = 0; i < L; ++i)
+                    if (src[i] >= S)
+                        throw Error(SVH_E_RANGE, "symbol " + std::to_string(src[i]) + " out of range (emit_num " +
+                                                     std::to_string(S) + ")");
         }
         // zero padding after the sequence (kSymPad and the 16-byte round-up)
         const uint64_t end = q + 1 < nseq ? h_symoff[q + 1] : bytes;

@@ -281,7 +281,10 @@ struct Batch {
     Batch(Model* m, uint64_t nseq, const uint64_t* offsets, const uint64_t* symbols, uint32_t flags);
     Batch(Model* m, uint64_t nseq, const uint64_t* offsets, const uint8_t* symbols, uint32_t flags);
     // replace the sequences (same flags); uploads are asynchronous on s
-    void load(uint64_t nseq, const uint64_t* offsets, const uint64_t* sym64, const uint8_t* sym8, hipStream_t s);
+    // (symbols from one packed array, sym64 or sym8, at `offsets`; or, with seqp, sequence q at
+    //  seqp[q] with length offsets[q+1] - offsets[q])
+    void load(uint64_t nseq, const uint64_t* offsets, const uint64_t* sym64, const uint8_t* sym8, hipStream_t s,
+              const uint64_t* const* seqp = nullptr);
     ~Batch();
     void run(uint32_t level, hipStream_t s);
     void read(hipStream_t s, float* scores, int64_t* best, int32_t* paths);

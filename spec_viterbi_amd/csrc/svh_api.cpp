@@ -287,16 +287,43 @@ int svh_batch_destroy(svh_batch_t b) {
     return guarded([&] { delete b; });
 }
 
+namespace {
+// svh_viterbi*: the model's kept batch (scores only / with paths), reloaded from the caller's
+// symbols in whichever form they come, then one run and one read (throws; callers guard)
+void oneshot(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* offsets, const uint64_t* sym64,
+             const uint8_t* sym8, const uint64_t* const* seqp, float* scores, int64_t* best_state, int32_t* paths) {
+    require(m != nullptr, "null model");
+    require(offsets && (sym64 || sym8 || seqp), "null offsets/symbols");
+    std::lock_guard<std::mutex> lock(m->oneshot_mu);
+    std::unique_ptr<svh::Batch>& b = m->oneshot[paths ? 1 : 0];
+    if (!b) {  // created once with a one-symbol placeholder; the load below replaces it
+        static const uint64_t one[2] = {0, 1};
+        static const uint8_t zero = 0;
+        b = std::make_unique<svh::Batch>(m->impl.get(), 1, one, &zero, paths ? SVH_BATCH_PATHS : 0u);
+    }
+    b->load(nseq, offsets, sym64, sym8, m->impl->stream, seqp);
+    b->run(level, nullptr);
+    b->read(nullptr, scores, best_state, paths);
+}
+}  // namespace
+
 int svh_viterbi(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* offsets,
                 const uint64_t* symbols, float* scores, int64_t* best_state, int32_t* paths) {
+    return guarded([&] { oneshot(m, level, nseq, offsets, symbols, nullptr, nullptr, scores, best_state, paths); });
+}
+
+int svh_viterbi_u8(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* offsets,
+                   const uint8_t* symbols, float* scores, int64_t* best_state, int32_t* paths) {
+    return guarded([&] { oneshot(m, level, nseq, offsets, nullptr, symbols, nullptr, scores, best_state, paths); });
+}
+
+int svh_viterbi_seqs(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* const* seqs,
+                     const uint64_t* lens, float* scores, int64_t* best_state, int32_t* paths) {
     return guarded([&] {
-        require(m != nullptr, "null model");
-        std::lock_guard<std::mutex> lock(m->oneshot_mu);
-        std::unique_ptr<svh::Batch>& b = m->oneshot[paths ? 1 : 0];
-        if (b) b->load(nseq, offsets, symbols, nullptr, m->impl->stream);
-        else b = std::make_unique<svh::Batch>(m->impl.get(), nseq, offsets, symbols, paths ? SVH_BATCH_PATHS : 0u);
-        b->run(level, nullptr);
-        b->read(nullptr, scores, best_state, paths);
+        require(seqs && lens, "null sequences/lengths");
+        std::vector<uint64_t> offs(nseq + 1, 0);
+        for (uint64_t q = 0; q < nseq; ++q) offs[q + 1] = offs[q] + lens[q];
+        oneshot(m, level, nseq, offs.data(), nullptr, nullptr, seqs, scores, best_state, paths);
     });
 }
 

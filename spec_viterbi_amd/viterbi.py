@@ -61,17 +61,45 @@ class DeviceModel:
         return DeviceBatch(self, seqs, paths)
 
     def viterbi(self, seqs, level: int = 0, paths: bool = False):
-        """One-shot: scores [nseq, n] (+ best state [nseq], + paths list if requested)."""
-        offsets, symbols = pack_sequences(seqs)
+        """One-shot: scores [nseq, n] (+ best state [nseq], + paths list if requested).
+        uint64 sequences go to svh_viterbi_seqs as they are (no flattening here: the C side narrows
+        each one straight into its pinned upload); anything else is packed first."""
+        seqs = [s if isinstance(s, np.ndarray) and s.dtype == np.uint64 and s.flags.c_contiguous
+                else np.ascontiguousarray(s, np.uint64) for s in seqs]
+        nseq = len(seqs)
+        lens = np.fromiter((s.size for s in seqs), np.uint64, nseq)
+        ptrs = np.fromiter((s.ctypes.data for s in seqs), np.uint64, nseq)
+        scores = np.empty((nseq, self.n), np.float32)
+        best = np.empty(nseq, np.int64)
+        pth = np.empty(int(lens.sum()), np.int32) if paths else None
+        _lib.check(_lib.lib.svh_viterbi_seqs(self._h, int(level), nseq, _p(ptrs, _u64), _p(lens, _u64),
+                                             _p(scores, _f32), _p(best, _i64), _p(pth, _i32) if paths else None))
+        if paths:
+            offsets = np.zeros(nseq + 1, np.int64)
+            np.cumsum(lens, out=offsets[1:])
+            return scores, best, [pth[offsets[q]:offsets[q + 1]] for q in range(nseq)]
+        return scores, best
+
+    def viterbi_packed(self, offsets, symbols, level: int = 0, paths: bool = False):
+        """One-shot over packed sequences: offsets [nseq+1] and uint8 symbols (the device format,
+        svh_viterbi_u8; e.g. what svh_reader_next returns) or uint64 symbols (svh_viterbi)."""
+        offsets = np.ascontiguousarray(offsets, np.uint64)
         nseq = offsets.size - 1
         scores = np.empty((nseq, self.n), np.float32)
         best = np.empty(nseq, np.int64)
-        pth = np.empty(int(offsets[-1]), np.int32) if paths else None
-        _lib.check(_lib.lib.svh_viterbi(self._h, int(level), nseq, _p(offsets, _u64), _p(symbols, _u64),
-                                        _p(scores, _f32), _p(best, _i64),
-                                        _p(pth, _i32) if paths else None))
+        pth = np.empty(int(offsets[-1] - offsets[0]) if nseq else 0, np.int32) if paths else None
+        symbols = np.asarray(symbols)
+        if symbols.dtype == np.uint8:
+            symbols = np.ascontiguousarray(symbols)
+            fn, sp = _lib.lib.svh_viterbi_u8, _p(symbols, ctypes.POINTER(ctypes.c_uint8))
+        else:
+            symbols = np.ascontiguousarray(symbols, np.uint64)
+            fn, sp = _lib.lib.svh_viterbi, _p(symbols, _u64)
+        _lib.check(fn(self._h, int(level), nseq, _p(offsets, _u64), sp, _p(scores, _f32), _p(best, _i64),
+                      _p(pth, _i32) if paths else None))
         if paths:
-            return scores, best, [pth[offsets[q]:offsets[q + 1]] for q in range(nseq)]
+            base = int(offsets[0])
+            return scores, best, [pth[int(offsets[q]) - base:int(offsets[q + 1]) - base] for q in range(nseq)]
         return scores, best
 
     def close(self):
