@@ -17,7 +17,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) \
 HOSTFLAGS := --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall
 
 HIP_SRCS  := $(wildcard $(CSRC)/fused_*.hip) $(CSRC)/misc.hip $(CSRC)/band.hip $(wildcard $(CSRC)/chain_*.hip) $(CSRC)/timepar.hip $(CSRC)/pipe.hip \
-             $(CSRC)/pipe_wide.hip $(CSRC)/pipe_paths.hip
+             $(CSRC)/pipe_tm1.hip $(CSRC)/pipe_tm1p.hip $(CSRC)/pipe_wide.hip $(CSRC)/pipe_paths.hip
 HOST_SRCS := $(CSRC)/runtime.cpp $(CSRC)/svh_api.cpp $(CSRC)/HIP_impl.cpp $(CSRC)/data_reader.cpp $(CSRC)/stream.cpp \
              $(CSRC)/seqreader.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS))
@@ -47,11 +47,13 @@ $(LIB): $(OBJS) $(BUILD)/pipe.hazards
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
 # The pipelined kernel's inline-asm DPP reads rely on the schedule for one of their two wait
-# states: every build checks all of them in the gfx950 code object (tools/dpp_hazards.py).
-$(BUILD)/pipe.hazards: $(BUILD)/pipe.o tools/dpp_hazards.py
-	cd $(BUILD) && /opt/rocm/lib/llvm/bin/llvm-objdump --offloading pipe.o > /dev/null
-	/opt/rocm/lib/llvm/bin/llvm-objdump -d $(BUILD)/pipe.o.0.hipv4-amdgcn-amd-amdhsa--gfx950 > $(BUILD)/pipe.s
-	python3 tools/dpp_hazards.py $(BUILD)/pipe.s pipe_viterbi_kernel > $@
+# states: every build checks all of them in the gfx950 code objects (tools/dpp_hazards.py).
+PIPE_OBJS := pipe pipe_tm1 pipe_tm1p
+$(BUILD)/pipe.hazards: $(foreach o,$(PIPE_OBJS),$(BUILD)/$(o).o) tools/dpp_hazards.py
+	set -e; for o in $(PIPE_OBJS); do \
+	  (cd $(BUILD) && /opt/rocm/lib/llvm/bin/llvm-objdump --offloading $$o.o > /dev/null); \
+	  /opt/rocm/lib/llvm/bin/llvm-objdump -d $(BUILD)/$$o.o.0.hipv4-amdgcn-amd-amdhsa--gfx950 > $(BUILD)/$$o.s; \
+	  python3 tools/dpp_hazards.py $(BUILD)/$$o.s pipe_viterbi_kernel; done > $@
 
 # Oracle: plain C, every add rounded on its own (test infrastructure only).
 $(ORACLE): oracle/viterbi_oracle.c oracle/viterbi_oracle.h

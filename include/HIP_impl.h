@@ -3,8 +3,9 @@
 // Drops in beside GraphBLAS_impl (reference: Viterbi_impl/GraphBLAS_impl.h:5-9, implementation
 // GraphBLAS_impl.cpp:4-93): same virtual, same result (final -log2 score per state, +inf for
 // unreachable states, bit-identical to GraphBLAS_impl's association).  Unlike the reference,
-// the model is uploaded to HBM once and cached per HMM (content-fingerprinted), not rebuilt on
-// every call.
+// the model is uploaded to HBM once and cached, not rebuilt on every call: each call compares the
+// HMM it is given field by field with a host copy of the one the cached model was built from
+// (memcmp of every vector), so a different or modified HMM rebuilds it.
 //
 // Error behaviour: the reference leaves an empty sequence / out-of-range symbol undefined; here
 // they throw std::invalid_argument / std::out_of_range.  HIP failures throw std::runtime_error.

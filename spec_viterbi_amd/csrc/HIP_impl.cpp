@@ -87,14 +87,16 @@ HMM::Mod_prob_vec_t run_one(svh_model_t m, uint64_t n, uint32_t level, const HMM
 
 std::vector<HMM::Mod_prob_vec_t> run_batch(svh_model_t m, uint64_t n, uint32_t level,
                                            const HMM::Emit_seq_vec_t& seqs) {
-    std::vector<uint64_t> offsets(seqs.size() + 1, 0);
-    for (size_t q = 0; q < seqs.size(); ++q) offsets[q + 1] = offsets[q] + seqs[q].size();
-    std::vector<uint64_t> symbols;
-    symbols.reserve(offsets.back());
-    for (const auto& s : seqs) symbols.insert(symbols.end(), s.begin(), s.end());
+    // the sequences as they are (Emit_t is size_t = uint64_t): no flattened copy on this side
+    static_assert(sizeof(HMM::Emit_t) == sizeof(uint64_t), "Emit_t must be 64-bit");
+    std::vector<const uint64_t*> ptrs(seqs.size());
+    std::vector<uint64_t> lens(seqs.size());
+    for (size_t q = 0; q < seqs.size(); ++q) {
+        ptrs[q] = reinterpret_cast<const uint64_t*>(seqs[q].data());
+        lens[q] = seqs[q].size();
+    }
     std::vector<float> scores(seqs.size() * n);
-    check(svh_viterbi(m, level, seqs.size(), offsets.data(), symbols.data(), scores.data(), nullptr,
-                      nullptr));
+    check(svh_viterbi_seqs(m, level, seqs.size(), ptrs.data(), lens.data(), scores.data(), nullptr, nullptr));
     std::vector<HMM::Mod_prob_vec_t> out(seqs.size());
     for (size_t q = 0; q < seqs.size(); ++q)
         out[q].assign(scores.begin() + q * n, scores.begin() + (q + 1) * n);

@@ -208,6 +208,7 @@ struct PipeModel {
     uint32_t n, S, P, nblk, SM, W, G;  // P = nblk*64*SM positions, G workgroups per sequence
     uint32_t cus;           // wide plan: CUs of the device (W = waves per workgroup at most)
     uint32_t sx;            // S has a term from F
+    uint32_t tm;            // latency plan's table mode (pipe_kernel.h): 1 = pair tables (SM = 2, S <= 20)
     // decoded paths (pipe PATHS variant + pipe_traceback_kernel):
     const uint8_t* pflags;  // [P] bit0: term from position p-1 exists, bit1: term from F exists,
                             // bit2: F's row < row of p-1 (F wins ties)
@@ -230,9 +231,11 @@ struct PipeScratch {
     uint32_t* viol;   // [rows] 1: speculation failed, row needs the serial kernel
     uint32_t rows, G;
 };
+constexpr uint32_t kPairSymbols = 20;  // pipe_kernel.h kPairSym: the pair tables' symbol capacity
 __host__ __device__ inline size_t pipe_lds_bytes(uint32_t W, uint32_t S) {
     // boundary ring [W][kPipeRing][64] | counters [16] | heavy constants [S][8] | reduction [W][4] | ticket
-    return ((size_t)W * kPipeRing * 64 + 16 + (size_t)S * 8 + (size_t)W * 4 + 4) * 4;
+    // | [3] pad | counter-publish sink [W][64] (lanes 1..63 of a count store write there)
+    return ((size_t)W * kPipeRing * 64 + 16 + (size_t)S * 8 + (size_t)W * 4 + 4 + (size_t)W * 64) * 4;
 }
 bool pipe_supported(int sm, int waves, bool sx);
 // b.cmask != nullptr selects the decoded-path variant (every sequence must start at step 0).

@@ -1,0 +1,20 @@
+// Pipelined chain Viterbi kernel, TM = 1 (pair tables read by 64-bit moves; pipe_kernel.h):
+// decoded-path instantiations (PATHS 1 and 2), 2 slots per lane, 4 waves per workgroup.
+#include "pipe_kernel.h"
+
+namespace svh {
+
+const void* pipe_kernel_tm1_paths(int sm, int waves, bool sx, int paths) {
+#ifdef SVH_PIPE_AB_ONLY
+    return nullptr;
+#else
+    if (sm != 2 || waves != 4 || paths < 1 || paths > 2) return nullptr;
+    if (paths == 2)
+        return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 2, 1>)
+                  : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 2, 1>);
+    return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 1, 1>)
+              : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 1, 1>);
+#endif
+}
+
+}  // namespace svh

@@ -224,8 +224,9 @@ class Viterbi_spec_impl(abc.ABC):
 
 
 def hmm_fingerprint(hmm: HMM) -> bytes:
-    """Content digest of an HMM (every field the device model is built from), the Python
-    counterpart of HIP_impl.cpp's fingerprint: equal digests <=> the same device model."""
+    """Content digest of an HMM (every field the device model is built from): equal digests <=>
+    the same device model.  The C++ HIP_impl compares a host copy field by field instead
+    (HIP_impl.cpp ModelKey); both rebuild the model for a different or modified HMM."""
     h = hashlib.blake2b(digest_size=16)
     h.update(np.array([hmm.states_num, hmm.emit_num], np.uint64).tobytes())
     for a in (hmm.trans_rows, hmm.trans_cols, hmm.trans_probs, hmm.emissions, hmm.start_probabilities_cols,

@@ -459,3 +459,45 @@ def test_oneshot_batches_reused_across_calls():
     scores, _ = model.viterbi(seqs[:7], level=1)
     for q in range(7):
         assert bit_equal(scores[q], ref[q]), q
+
+
+def test_oneshot_symbol_forms_agree():
+    """The three one-shot entry points -- separate uint64 arrays (svh_viterbi_seqs, what
+    DeviceModel.viterbi and HIP_impl::run_Viterbi_batch call), packed uint64 (svh_viterbi) and
+    packed uint8 (svh_viterbi_u8, the device format) -- give the oracle's scores, best states and
+    paths, and the same error codes (out-of-range symbol, empty sequence, null pointers)."""
+    import ctypes
+
+    from spec_viterbi_amd.hmm import pack_sequences
+
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = [s[:L] for s, L in zip(svh.read_emit_seq(ess("covid-19.ess")), (1, 2, 31, 32, 33, 900, 1025, 64))]
+    model = svh.DeviceModel(hmm)
+    offs, sym64 = pack_sequences(seqs)
+    got = {"seqs": model.viterbi(seqs, paths=True), "u64": model.viterbi_packed(offs, sym64, paths=True),
+           "u8": model.viterbi_packed(offs, sym64.astype(np.uint8), paths=True)}
+    for q, s in enumerate(seqs):
+        r, rb, rp = oracle.decode(hmm, s)
+        for name, (scores, best, pth) in got.items():
+            assert bit_equal(scores[q], r) and best[q] == rb and np.array_equal(pth[q], rp), (name, q)
+    # a list of non-uint64 arrays is converted, then runs the same path
+    s32 = [np.asarray(s, np.int32) for s in seqs[:3]]
+    assert all(bit_equal(a, b) for a, b in zip(model.viterbi(s32)[0], got["seqs"][0][:3]))
+    bad = np.array([0, 1, 20], np.uint64)  # 20 >= emit_num
+    for call in (lambda: model.viterbi([bad]),
+                 lambda: model.viterbi_packed(np.array([0, 3], np.uint64), bad),
+                 lambda: model.viterbi_packed(np.array([0, 3], np.uint64), bad.astype(np.uint8))):
+        with pytest.raises(_lib.SvhError) as e:
+            call()
+        assert e.value.code == _lib.SVH_E_RANGE
+    with pytest.raises(_lib.SvhError) as e:
+        model.viterbi([seqs[0], np.array([], np.uint64)])
+    assert e.value.code == _lib.SVH_E_INVALID
+    lens = np.array([3], np.uint64)
+    ptrs = np.zeros(1, np.uint64)
+    rc = _lib.lib.svh_viterbi_seqs(model.handle, 0, 1, ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                  lens.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), None, None, None)
+    assert rc == _lib.SVH_E_INVALID  # a null sequence pointer
+    # and the model still answers afterwards
+    scores, best = model.viterbi(seqs)
+    assert all(bit_equal(scores[q], got["seqs"][0][q]) for q in range(len(seqs)))
