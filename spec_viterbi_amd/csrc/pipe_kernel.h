@@ -114,6 +114,32 @@ __device__ __forceinline__ void lds_put1(uint32_t addr, uint32_t v) {
         : "memory");
 }
 
+// The chain term of slot 0 alone (TM = 2, whose feeder terms come out of the indexed block):
+// xb = fl(eb + (lane ? x[lane-1] : b)), b the SGPR boundary (R < 0), lane 0 of bvv (R = 0) or lane R
+// of bvv (row_ror:16-R).  x was written before the step's indexed block and bvv at the start of
+// the group, so both DPP reads have their wait states (tools/dpp_hazards.py checks every build).
+template <int R>
+__device__ __forceinline__ float chain_b(float eb, float b, float x) {
+    float xb;
+    if constexpr (R < 0) {
+        asm("v_add_f32_e32 %0, %1, %2\n\t"
+            "v_add_f32_dpp %0, %3, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb)
+            : "s"(b), "v"(eb), "v"(x));
+    } else if constexpr (R == 0) {
+        asm("v_add_f32_e32 %0, %1, %2\n\t"
+            "v_add_f32_dpp %0, %3, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb)
+            : "v"(b), "v"(eb), "v"(x));
+    } else {
+        asm("v_add_f32_dpp %0, %1, %2 row_ror:%4 row_mask:0xf bank_mask:0xf\n\t"
+            "v_add_f32_dpp %0, %3, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb)
+            : "v"(b), "v"(eb), "v"(x), "n"(16 - R));
+    }
+    return xb;
+}
+
 // Chain and feeder terms of slot 0: xb = fl(eb + (lane ? x[lane-1] : bnd)), xa = fl(ea + f).
 // The DPP read of x follows two VALU instructions of this block (its two wait states).
 __device__ __forceinline__ void chain_terms(float& xb, float& xa, float eb, float ea, float bnd, float f,
@@ -177,6 +203,7 @@ struct ChainIn {
 template <int SM, int W, bool SX, int PATHS, int TM>
 __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     static_assert(TM == 0 || SM == 2, "pair tables: two slots per lane");
+    static_assert(TM >= 0 && TM <= 2, "table mode");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* ring = lds;                                                  // [W][kR][64]
     uint32_t* cnt = reinterpret_cast<uint32_t*>(ring + W * kR * 64);    // [16]
@@ -250,7 +277,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 EA[s][o] = (uint32_t)o < S ? e.y : kInf;
             }
         // mode 3: the pair-interleaved tables (symbols >= S: +inf)
-        constexpr bool kT3 = TM == 1;  // pair tables (symbols pre-doubled)
+        constexpr bool kT3 = TM >= 1;  // pair tables (symbols pre-doubled)
         constexpr bool kT4 = TM == 1;  // ... read by four 64-bit moves
         f32x32 TA[4];
         f32x8 TB[4];
@@ -442,7 +469,52 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         auto step = [&](uint32_t o, auto in) {
             constexpr int R = decltype(in)::value;
             float xa[SM], xb[SM];  // feeder and chain terms of every slot
-            if constexpr (kT4) {  // o is 2 x the symbol: four 64-bit moves out of the pair tables
+            if constexpr (TM == 2) {  // o is 2 x the symbol: the table reads are indexed operands
+                // of the adds that use them (one gpr_idx(SRC0) block; only eb_0 is moved out, for
+                // slot 0's DPP chain add)
+                const float pm = fminf(v[0], v[1]);  // the heavy side reads the scores of t-1
+                f2 pmv;  // the packed add reads the low half twice (op_sel_hi): the high half is never read
+                pmv.x = pm;
+                float eb0;
+                f2 s1, s2;  // {A_S + m, A_F + m}, {X_SS + c, X_FF + F}
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+#pragma clang diagnostic ignored "-Wuninitialized"
+                asm("s_set_gpr_idx_on %[o], gpr_idx(SRC0)\n\t"
+                    "v_mov_b32 %[eb0], v2\n\t"
+                    "v_add_f32 %[xa0], v3, %[f]\n\t"
+                    "v_add_f32 %[xa1], v43, %[f]\n\t"
+                    "v_add_f32 %[xb1], v42, %[v0]\n\t"
+                    "v_pk_add_f32 %[s1], v[82:83], %[pm] op_sel_hi:[1,0]\n\t"
+                    "v_pk_add_f32 %[s2], v[122:123], %[cf]\n\t"
+                    "s_set_gpr_idx_off"
+                    : [eb0] "=&v"(eb0), [xa0] "=&v"(xa[0]), [xa1] "=&v"(xa[1]), [xb1] "=&v"(xb[1]), [s1] "=&v"(s1),
+                      [s2] "=&v"(s2)
+                    : [o] "s"(o), [f] "v"(CF.y), [v0] "v"(v[0]), [pm] "v"(pmv), [cf] "v"(CF), "{v[2:33]}"(TA[0]),
+                      "{v[34:41]}"(TB[0]), "{v[42:73]}"(TA[1]), "{v[74:81]}"(TB[1]), "{v[82:113]}"(TA[2]),
+                      "{v[114:121]}"(TB[2]), "{v[122:153]}"(TA[3]), "{v[154:161]}"(TB[3])
+                    : "m0");
+#pragma clang diagnostic pop
+                xb[0] = chain_b<R>(eb0, in.b, v[1]);
+                float cn = fminf(s1.x, s2.x);
+                if constexpr (SX) cn = fminf(cn, readlane_f(cXSF, o >> 1) + CF.y);
+                asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+                             : "+v"(viol)
+                             : "v"(s1.y), "v"(s2.y)
+                             : "vcc");
+                auto push = [&](int s, float a, float bb) {
+                    if constexpr (PATHS == 2) push_le(macc[s], a, bb);
+                    else if constexpr (PATHS == 1) push_lt_eqc(macc[s], a, bb, pmC[s]);
+                };
+                if constexpr (PATHS) last_pm = pm;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    if constexpr (PATHS) push(s, xa[s], xb[s]);
+                    v[s] = fminf(xa[s], xb[s]);
+                }
+                CF = (f2){cn, s2.y};
+                return;
+            } else if constexpr (kT4) {  // o is 2 x the symbol: four 64-bit moves out of the pair tables
                 f2 p0, p1, kS, kX;  // {eb_0, ea_0}, {eb_1, ea_1}, {A_S, A_F}, {X_SS, X_FF}
                 // M0 is reserved (clang warns on the clobber); the kernel uses it nowhere else
 #pragma clang diagnostic push

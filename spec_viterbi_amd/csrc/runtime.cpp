@@ -781,7 +781,10 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     // the pair-table step (pipe_kernel.h TM = 1) wherever it applies; SVH_PIPE_TM=0 forces the
     // per-slot tables (A/B and tests)
     view.tm = !p.wide && p.SM == 2 && p.W == 4 && S <= kPairSymbols ? 1u : 0u;
-    if (const char* e = std::getenv("SVH_PIPE_TM"); e && std::atoi(e) == 0) view.tm = 0;
+    if (const char* e = std::getenv("SVH_PIPE_TM"); e) {  // A/B: 0 per-slot tables, 2 indexed operands
+        const int t = std::atoi(e);
+        if (t == 0 || (t == 2 && view.tm)) view.tm = (uint32_t)t;
+    }
     if (const char* e = std::getenv("SVH_PIPE_DEBUG"); e && std::atoi(e)) {  // diagnostics only
         d_stamps.alloc((size_t)65536 * kPipeStamps * 8);
         hip_check(hipMemsetAsync(d_stamps.ptr, 0, d_stamps.bytes, s), "stamps");

@@ -45,7 +45,6 @@ __device__ __forceinline__ float chain_b(float eb, float bvv, float x) {
     float xb;
     if constexpr (R == 0) {
         asm("v_add_f32_e32 %0, %1, %2\n\t"
-            "s_nop 0\n\t"
             "v_add_f32_dpp %0, %3, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
             : "=&v"(xb)
             : "v"(bvv), "v"(eb), "v"(x));
@@ -148,6 +147,35 @@ __global__ __launch_bounds__(256) void steps(const float* tab, const uint8_t* sy
             chain_terms_v<R>(xb[0], xa[0], eb[0], ea[0], bv, CF.y, v[1]);
             xa[1] = ea[1] + CF.y;
             xb[1] = eb[1] + v[0];
+        } else if constexpr (V == 7) {  // indexed operands in one SRC0 block (pair tables)
+            const float pm0 = fminf(v[0], v[1]);
+            f2 pmv;  // the packed add reads the low half twice (op_sel_hi): the high half stays undefined
+            pmv.x = pm0;
+            float eb0;
+            f2 s1v, s2v;
+            asm volatile("s_set_gpr_idx_on %[o], gpr_idx(SRC0)\n\t"
+                         "v_mov_b32 %[eb0], v2\n\t"
+                         "v_add_f32 %[xa0], v3, %[f]\n\t"
+                         "v_add_f32 %[xa1], v43, %[f]\n\t"
+                         "v_add_f32 %[xb1], v42, %[v0]\n\t"
+                         "v_pk_add_f32 %[s1], v[82:83], %[pm] op_sel_hi:[1,0]\n\t"
+                         "v_pk_add_f32 %[s2], v[122:123], %[cf]\n\t"
+                         "s_set_gpr_idx_off"
+                         : [eb0] "=&v"(eb0), [xa0] "=&v"(xa[0]), [xa1] "=&v"(xa[1]), [xb1] "=&v"(xb[1]),
+                           [s1] "=&v"(s1v), [s2] "=&v"(s2v)
+                         : [o] "s"(2 * o), [f] "v"(CF.y), [v0] "v"(v[0]), [pm] "v"(pmv), [cf] "v"(CF), TAB_IN
+                         : "m0");
+            xb[0] = chain_b<R>(eb0, bv, v[1]);
+            const float n0 = fminf(xa[0], xb[0]), n1 = fminf(xa[1], xb[1]);
+            const float cn = fminf(s1v.x, s2v.x);
+            asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+                         : "+v"(viol)
+                         : "v"(s1v.y), "v"(s2v.y)
+                         : "vcc");
+            CF = (f2){cn, s2v.y};
+            v[0] = n0;
+            v[1] = n1;
+            return;
         } else {
             f2 p0, p1;
             if constexpr (V == 4) {  // eight 32-bit moves
@@ -192,7 +220,7 @@ __global__ __launch_bounds__(256) void steps(const float* tab, const uint8_t* sy
         const f2 s1 = kS + (f2){pm, pm};
         const f2 s2 = kX + CF;
         const float cn = fminf(s1.x, s2.x);
-        if constexpr (V <= 1 || V == 6) {
+        if constexpr (V <= 1 || V >= 6) {
             asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
                          : "+v"(viol)
                          : "v"(s1.y), "v"(s2.y)
@@ -224,7 +252,7 @@ __global__ __launch_bounds__(256) void steps(const float* tab, const uint8_t* sy
                 const uint32_t o = (uint32_t)((sw[j] >> (8 * k)) & 0xFFu);
                 if constexpr (k == 0) step(o, std::integral_constant<int, 7>{}, bv_prev);
                 else step(o, std::integral_constant<int, (int)k - 1>{}, bv);
-                if constexpr (V != 3 && V != 6) ring[(8 * j + k) * 64 + lane] = v[1];
+                if constexpr (V != 3 && V != 6 && V != 8) ring[(8 * j + k) * 64 + lane] = v[1];
             };
             one(std::integral_constant<uint32_t, 0>{});
             one(std::integral_constant<uint32_t, 1>{});
@@ -243,7 +271,7 @@ __global__ __launch_bounds__(256) void steps(const float* tab, const uint8_t* sy
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (lane == 0) cyc[gw] = t1 - t0;
-    const bool bad = V <= 1 || V == 6 ? viol != 0 : vmin < 0.0f;
+    const bool bad = V <= 1 || V >= 6 ? viol != 0 : vmin < 0.0f;
     St* o = reinterpret_cast<St*>(out) + gw * 64 + lane;
     o->v0 = v[0];
     o->v1 = v[1];
@@ -299,11 +327,12 @@ int main(int argc, char** argv) {
                            "V3 V2 without ds_write",
                            "V4 8x v_mov_b32 pair tables, sub/min, ds_write",
                            "V5 V2 + packed xa pair",
-                           "V6 V0 without ds_write"};
+                           "V6 V0 without ds_write",
+                           "V7 indexed operands in one SRC0 block, ds_write"};
     std::vector<St> ref, got;
-    double c[7];
+    double c[8];
     c[0] = run<0>(dtab, dsym, dout, dcyc, groups, blocks, ref);
-    bool same[7] = {true};
+    bool same[8] = {true};
     auto cmp = [&](int i) {
         same[i] = true;
         for (size_t k = 0; k < ref.size(); ++k)
@@ -318,9 +347,10 @@ int main(int argc, char** argv) {
     c[4] = run<4>(dtab, dsym, dout, dcyc, groups, blocks, got), cmp(4);
     c[5] = run<5>(dtab, dsym, dout, dcyc, groups, blocks, got), cmp(5);
     c[6] = run<6>(dtab, dsym, dout, dcyc, groups, blocks, got), cmp(6);
+    c[7] = run<7>(dtab, dsym, dout, dcyc, groups, blocks, got), cmp(7);
     const hipError_t e = hipDeviceSynchronize();
     std::printf("status %s, %d workgroup(s) of 4 waves, %d observations\n", hipGetErrorString(e), blocks, groups * 32);
-    for (int i = 0; i < 7; ++i)
+    for (int i = 0; i < 8; ++i)
         std::printf("%-52s %7.1f cycles/obs  %s\n", names[i], c[i], same[i] ? "same state" : "DIFFERS");
     std::printf("ref lane0: v0 %g v1 %g c %g F %g viol %g\n", ref[0].v0, ref[0].v1, ref[0].cx, ref[0].cy, ref[0].extra);
     return 0;
