@@ -18,3 +18,7 @@ done
 timeout -k 10 60 tools/ubench/step_ubench 250 > $OUT/step_ubench.txt 2>&1 && cat $OUT/step_ubench.txt
 timeout -k 10 120 python3 tools/e2e_split.py > $OUT/e2e_split.json 2>&1 || { cat $OUT/e2e_split.json; exit 1; }
 cat $OUT/e2e_split.json
+for sh in covid emit50; do
+    timeout -k 10 120 python3 tools/shard_shares.py --shard $sh > $OUT/shares_$sh.json 2>&1 || { cat $OUT/shares_$sh.json; exit 1; }
+    python3 -c "import json;d=json.load(open('$OUT/shares_$sh.json'));print('$sh', {k:(v['makespan_ms'],v['forecast_speedup']) for k,v in d['ranks'].items()})"
+done
