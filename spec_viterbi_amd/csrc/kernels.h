@@ -209,6 +209,7 @@ struct PipeModel {
     uint32_t cus;           // wide plan: CUs of the device (W = waves per workgroup at most)
     uint32_t sx;            // S has a term from F
     uint32_t tm;            // latency plan's table mode (pipe_kernel.h): 1 = pair tables (SM = 2, S <= 20)
+    uint32_t wide;          // 1: the wide plan's geometry and table layout (pipe_wide_kernel.h)
     // decoded paths (pipe PATHS variant + pipe_traceback_kernel):
     const uint8_t* pflags;  // [P] bit0: term from position p-1 exists, bit1: term from F exists,
                             // bit2: F's row < row of p-1 (F wins ties)
@@ -246,11 +247,16 @@ bool pipe_paths_supported(int sm, int waves);
 // to the chain traceback.
 hipError_t launch_pipe_traceback(const PipeModel& m, const FusedBatch& b, const uint64_t* path_off, int32_t* paths,
                                  const uint32_t* skip, hipStream_t stream);
+// Light positions the pipelined traceback stages in LDS (pipe_paths.hip): plans with more decode
+// paths on the chain kernel.
+constexpr uint32_t kPipeTbMaxP = 2560;
 // Per-sequence sizes of the decoded-path buffers of the pipelined plan.
 inline uint64_t pipe_mask_words(uint64_t len, uint32_t nblk, uint32_t sm) {
     return len > 1 ? (len - 1 + 31) / 32 * (uint64_t)nblk * sm * 64 : 0;
 }
-inline uint64_t pipe_prec_count(uint64_t len, uint32_t nblk) { return (uint64_t)nblk * 2 * len; }
+// heavy partials per block and observation: 2 (latency plan: one per half-wave), 1 (wide plan)
+__host__ __device__ inline uint32_t pipe_prec_parts(bool wide) { return wide ? 1u : 2u; }
+inline uint64_t pipe_prec_count(uint64_t len, uint32_t nblk, uint32_t parts) { return (uint64_t)nblk * parts * len; }
 inline uint64_t pipe_ckpt_floats(uint64_t len, uint32_t P) { return len ? ((len - 1) / kCkptEvery + 1) * (uint64_t)P : 0; }
 inline uint64_t pipe_fck_floats(uint64_t len) { return len ? (len - 1) / 32 + 1 : 0; }
 // LDS of the decoded-path variant beyond pipe_lds_bytes: a ring of 32 rows {pm, c} per wave
@@ -259,12 +265,16 @@ inline size_t pipe_path_lds_bytes(uint32_t W) { return (size_t)W * 32 * kPRingSt
 // Wide pipelined plan (pipe_wide.hip): one block of 64*SM positions per workgroup, W sequences
 // (one per wave), the block's table [nblk][S][NC][64] float4 in LDS (PipeModel.tab; G = nblk);
 // NC = SM/2 (eb|ea) chunks + {A_S A_F X_SS X_FF} [+ {X_SF 0 0 0} when sx], constants per lane.
-inline uint32_t pipew_chunks(uint32_t SM, bool sx) { return SM / 2 + 1 + (sx ? 1 : 0); }
-inline size_t pipew_lds_bytes(uint32_t SM, uint32_t W, uint32_t S, bool sx) {
-    // table [S][NC][64] float4 | boundary ring [W][8][64] | ticket
-    return (size_t)S * pipew_chunks(SM, sx) * 64 * 16 + (size_t)W * 8 * 64 * 4 + 16;
+__host__ __device__ inline uint32_t pipew_chunks(uint32_t SM, bool sx) { return SM / 2 + 1 + (sx ? 1 : 0); }
+inline size_t pipew_lds_bytes(uint32_t SM, uint32_t W, uint32_t S, bool sx, bool paths = false) {
+    // table [S][NC][64] float4 | boundary ring [W][8][64] | ticket | paths: ring [W][8][kPRingStride]
+    return (size_t)S * pipew_chunks(SM, sx) * 64 * 16 + (size_t)W * 8 * 64 * 4 + 16 +
+           (paths ? (size_t)W * 8 * kPRingStride * 4 : 0);
 }
 bool pipew_supported(int sm, int waves, bool sx);
+// Decoded paths on the wide plan: the most sequences per workgroup whose LDS fits (0: none).
+uint32_t pipew_paths_waves_max(uint32_t sm, uint32_t S, bool sx);
+bool pipew_paths_supported(int sm, uint32_t S, bool sx);
 // Sequences (waves) per workgroup of a wide launch over nseq rows: the fewest of 1, 2, 4, 8, 12,
 // 16 that give about one workgroup per CU (a workgroup holds a CU's LDS), at most m.W.
 inline uint32_t pipew_waves_for(const PipeModel& m, uint64_t nseq) {
@@ -278,6 +288,7 @@ inline uint32_t pipew_waves_for(const PipeModel& m, uint64_t nseq) {
         }
     return w;
 }
+// b.cmask != nullptr selects the decoded-path variant (every sequence must start at step 0).
 hipError_t launch_pipew(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
 
 // CSR of T^T used by the generic kernel and the _spec precompute.

@@ -24,7 +24,7 @@ using namespace pipe_dev;
 
 namespace {
 
-constexpr uint32_t kPTbMaxP = 2560;  // light positions the j* recompute stages in LDS (x2 buffers)
+constexpr uint32_t kPTbMaxP = kPipeTbMaxP;  // light positions the j* recompute stages in LDS (x2 buffers)
 constexpr uint32_t kPTbMaxN = kPTbMaxP + 2;  // states whose position map is staged in LDS
 
 __device__ __forceinline__ void wave_sync() {
@@ -78,6 +78,17 @@ struct RecSrc {
     __device__ float C(uint32_t r) const { return r ? reduce(r, 1) : c0; }
 };
 
+// (eb, ea) of position x for symbol o in the plan's table layout: the latency plan's
+// [nblk][S][SM][64] float2, or the wide plan's [nblk][S][NC][64] float4 chunks ([eb_1 .. eb_{SM-1},
+// eb_0] then [ea_0 .. ea_{SM-1}], pipe_wide_kernel.h).
+__device__ __forceinline__ float2 pipe_tab_pair(const PipeModel& m, uint32_t x, uint32_t o) {
+    const uint32_t SM = m.SM, bsz = 64 * SM, blk = x / bsz, ln = (x % bsz) / SM, s = x % SM;
+    if (!m.wide) return m.tab[(((size_t)blk * m.S + o) * SM + s) * 64 + ln];
+    const float* base = reinterpret_cast<const float*>(m.tab) + ((size_t)blk * m.S + o) * pipew_chunks(SM, m.sx != 0) * 256;
+    const uint32_t ib = s == 0 ? SM - 1 : s - 1, ia = SM + s;
+    return make_float2(base[((ib / 4) * 64 + ln) * 4 + ib % 4], base[((ia / 4) * 64 + ln) * 4 + ia % 4]);
+}
+
 // j* of record row r for heavy row h (0 = F, 1 = S): the lowest light position p with
 // fl(cA_h + v_r[p]) == fl(cA_h + mu_r), cA_h the light-set constant of h for the symbol of
 // observation r+1.  v_r is recomputed by one wave from the checkpoint row c = r rounded down to
@@ -85,7 +96,7 @@ struct RecSrc {
 // fl(eb_p + v_{i-1}[p-1])) (v_{i-1}[-1] = +inf), F advanced alongside from F(c).
 __device__ uint32_t pipe_jstar(const PipeModel& m, const RecSrc& rs, const float* ck, uint32_t r, uint32_t h,
                                float* buf) {
-    const uint32_t lane = threadIdx.x & 63u, P = m.P, SM = m.SM, bsz = 64 * SM;
+    const uint32_t lane = threadIdx.x & 63u, P = m.P;
     const uint32_t c = r / kCkptEvery * kCkptEvery;
     float* cur = buf;
     float* nxt = buf + kPTbMaxP;
@@ -96,8 +107,7 @@ __device__ uint32_t pipe_jstar(const PipeModel& m, const RecSrc& rs, const float
     for (uint32_t i = c + 1; i <= r; ++i) {
         const uint32_t o = rs.sym[i];
         for (uint32_t x = lane; x < P; x += 64) {
-            const uint32_t blk = x / bsz, ln = (x % bsz) / SM, s = x % SM;
-            const float2 e = m.tab[(((size_t)blk * m.S + o) * SM + s) * 64 + ln];
+            const float2 e = pipe_tab_pair(m, x, o);
             const float pv = x ? cur[x - 1] : kInf;
             nxt[x] = fminf(e.y + F, e.x + pv);
         }
@@ -148,7 +158,7 @@ __global__ __launch_bounds__(64) void pipe_traceback_kernel(PipeModel m, FusedBa
     rs.sym = b.symbols + b.sym_off[q];
     rs.hcl = hcl;
     rs.len = len;
-    rs.U = 2 * nblk;
+    rs.U = pipe_prec_parts(m.wide != 0) * nblk;
     wave_sync();
     rs.c0 = m.rowS >= 0 ? hcl[(size_t)rs.sym[0] * 8 + 6] + m.startS : kInf;
     // F's backpointer is itself wherever the kernel's check held (see above)

@@ -780,6 +780,7 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     view.sx = p.sx ? 1u : 0u;
     // the pair-table step (pipe_kernel.h TM = 1) wherever it applies; SVH_PIPE_TM=0 forces the
     // per-slot tables (A/B and tests)
+    view.wide = p.wide ? 1u : 0u;
     view.tm = !p.wide && p.SM == 2 && p.W == 4 && S <= kPairSymbols ? 1u : 0u;
     if (const char* e = std::getenv("SVH_PIPE_TM"); e) {  // A/B: 0 per-slot tables, 2 indexed operands
         const int t = std::atoi(e);
@@ -1071,12 +1072,21 @@ const DevicePipePlan* Model::pipe_for(uint32_t nseq) const {
     return nullptr;
 }
 
+// Decoded paths: the latency plan's path variant for the batches its scores pass takes, the wide
+// plan's beyond that (the chain kernel's path variant is the exact fallback of both, so the model
+// needs its plan too); SVH_PIPEW_PATHS=0 sends wide path batches to the chain kernel (A/B).
 const DevicePipePlan* Model::pipe_paths_for(uint32_t nseq) const {
-    if (!pipe.plan.ok || !pipe_paths_supported((int)pipe.plan.SM, (int)pipe.plan.W) || pipe.plan.P > 2560 ||
-        !band.plan.paths_ok())
-        return nullptr;
-    if (kernel_pref == SVH_KERNEL_PIPE) return &pipe;
-    if (kernel_pref == SVH_KERNEL_AUTO && nseq <= pipe_max_nseq) return &pipe;
+    if (!band.plan.paths_ok()) return nullptr;
+    const bool lat = pipe.plan.ok && pipe_paths_supported((int)pipe.plan.SM, (int)pipe.plan.W) &&
+                     pipe.plan.P <= kPipeTbMaxP;
+    static const bool wide_env = !(std::getenv("SVH_PIPEW_PATHS") && std::atoi(std::getenv("SVH_PIPEW_PATHS")) == 0);
+    const bool wid = wide_env && pipe_wide.plan.ok && pipe_wide.plan.P <= kPipeTbMaxP &&
+                     pipew_paths_supported((int)pipe_wide.plan.SM, host.S, pipe_wide.plan.sx);
+    if (kernel_pref == SVH_KERNEL_PIPE) return lat ? &pipe : nullptr;
+    if (kernel_pref == SVH_KERNEL_PIPE_WIDE) return wid ? &pipe_wide : nullptr;
+    if (kernel_pref != SVH_KERNEL_AUTO) return nullptr;
+    if (lat && nseq <= pipe_max_nseq) return &pipe;
+    if (wid && nseq >= pipew_min_nseq) return &pipe_wide;
     return nullptr;
 }
 
@@ -1164,17 +1174,19 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
     }
     i.spec_level = spec_level;
     i.spec_bytes = d_products.bytes;
-    i.paths_kernel = pipe_paths_for(1) ? SVH_KERNEL_PIPE
+    const DevicePipePlan* pp1 = pipe_paths_for(1);
+    i.paths_kernel = pp1 ? (pp1->plan.wide ? SVH_KERNEL_PIPE_WIDE : SVH_KERNEL_PIPE)
                      : band_for(true) ? SVH_KERNEL_CHAIN : plan_for(true) ? SVH_KERNEL_FUSED : SVH_KERNEL_GENERIC;
     i.wide_threads = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.B : 0;
     i.wide_slots = band_wide.plan.ok && band_for(false) ? (int32_t)band_wide.plan.SM : 0;
     i.cu_count = cu_count;
     if (ppl) {
-        const uint32_t w = ppl->plan.wide ? pipew_waves_for(ppl->view, nseq) : ppl->plan.W;
+        uint32_t w = ppl->plan.wide ? pipew_waves_for(ppl->view, nseq) : ppl->plan.W;
+        if (ppl->plan.wide && paths) w = std::min(w, pipew_paths_waves_max(ppl->plan.SM, host.S, ppl->plan.sx));
         i.kernel = ppl->plan.wide ? SVH_KERNEL_PIPE_WIDE : SVH_KERNEL_PIPE;
         i.threads = (int32_t)(64 * w);
         i.slots = (int32_t)ppl->plan.SM;
-        i.lds_bytes = ppl->plan.wide ? pipew_lds_bytes(ppl->plan.SM, w, host.S, ppl->plan.sx)
+        i.lds_bytes = ppl->plan.wide ? pipew_lds_bytes(ppl->plan.SM, w, host.S, ppl->plan.sx, paths)
                                      : pipe_lds_bytes(ppl->plan.W, host.S);
     }
     if (pipe_wide.plan.ok) {
@@ -1269,7 +1281,7 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
                 h_pmoff[q] = pmn;
                 pmn += pipe_mask_words(len, ppl->plan.nblk, ppl->plan.SM);
                 h_proff[q] = prn;
-                prn += pipe_prec_count(len, ppl->plan.nblk);
+                prn += pipe_prec_count(len, ppl->plan.nblk, pipe_prec_parts(ppl->plan.wide));
                 h_pcoff[q] = pcn;
                 pcn += pipe_ckpt_floats(len, ppl->plan.P);
                 h_fcoff[q] = fcn;
@@ -1474,7 +1486,8 @@ void Batch::run(uint32_t level, hipStream_t s) {
         pb.fck = d_fck.as<float>();
         pb.fck_off = p_fcoff;
         pb.pipe = &pipe.view;
-        hip_check(launch_pipe(ppl->view, pb, pipe.view, s), "pipelined Viterbi kernel (paths)");
+        if (ppl->plan.wide) hip_check(launch_pipew(ppl->view, pb, pipe.view, s), "wide pipelined Viterbi kernel (paths)");
+        else hip_check(launch_pipe(ppl->view, pb, pipe.view, s), "pipelined Viterbi kernel (paths)");
         FusedBatch cb = fb;  // chain buffers
         cb.run_mask = pipe.view.viol;
         hip_check(launch_chain(bpl->view, 1, cb, s), "chain Viterbi kernel (pipe paths fallback)");

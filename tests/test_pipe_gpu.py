@@ -377,14 +377,14 @@ def test_fallbacks_reset_by_time_parallel_run():
     model.close()
 
 
-# ---- decoded paths on the pipelined latency plan (pipe.hip PATHS + pipe_paths.hip) -------------
+# ---- decoded paths on the pipelined plans (pipe_kernel.h / pipe_wide_kernel.h PATHS + pipe_paths.hip)
 def decode_check(hmm, seqs, kernel=_lib.SVH_KERNEL_PIPE, expect_plan=True):
     """Scores, best states and paths of one decoded-path batch against the oracle's decode."""
     model = svh.DeviceModel(hmm, kernel=kernel)
     batch = model.batch(seqs, paths=True)
     plan = batch.plan()
     if expect_plan:
-        assert plan["kernel"] == _lib.SVH_KERNEL_PIPE, plan
+        assert plan["kernel"] == kernel, plan
     batch.run()
     s, b, pth = batch.read(want_paths=True)
     fb = batch.fallbacks()
@@ -425,49 +425,85 @@ def test_pipe_paths_headline_digests():
         model.close()
 
 
-@pytest.mark.parametrize("L", [1, 2, 3, 16, 17, 31, 32, 33, 34, 63, 64, 65, 97, 1025, 2049])
-def test_pipe_paths_sequence_lengths(L):
-    """Mask words (every 32 rows), checkpoints (every 16), ring folds (every 32 observations) and
-    the F checkpoints at every head / body / tail boundary; three workgroups per sequence."""
-    hmm = random_chain_hmm(700, S=20, seed=L, n_from_m=False)
-    decode_check(hmm, random_seqs(20, [L, L + 5, max(1, L - 3)], seed=L))
+@pipes
+@pytest.mark.parametrize("L", [1, 2, 3, 7, 8, 9, 16, 17, 31, 32, 33, 34, 63, 64, 65, 97, 1025, 2049])
+def test_pipe_paths_sequence_lengths(L, kern):
+    """Mask words (every 32 rows), checkpoints (every 16), ring folds (every 32 observations on the
+    latency plan, every 8 on the wide plan) and the F checkpoints at every head / body / tail
+    boundary; three workgroups (latency) or three blocks (wide) per sequence."""
+    hmm = random_chain_hmm(700 if kern == _lib.SVH_KERNEL_PIPE else 1300, S=20, seed=L, n_from_m=False)
+    decode_check(hmm, random_seqs(20, [L, L + 5, max(1, L - 3)], seed=L), kernel=kern)
 
 
 @pytest.mark.parametrize("variant", [dict(), dict(self_n=False), dict(c_from_m=False), dict(self_c=False),
                                      dict(gap=37), dict(zero_emis=0.2), dict(ties=True), dict(inf_edges=0.1),
                                      dict(start=(0, 5, 301)), dict(n_from_m=False)])
-def test_pipe_paths_chain_variants(variant):
+@pipes
+def test_pipe_paths_chain_variants(variant, kern):
     """MSV-shaped random models (ties, chain breaks, +inf edges, starts in light rows, no self
     loops): scores, best states and every path entry equal to the oracle's decode."""
     hmm = random_chain_hmm(600, S=12, seed=11, **variant)
-    decode_check(hmm, random_seqs(12, [300, 64, 1, 97, 700], seed=12))
+    decode_check(hmm, random_seqs(12, [300, 64, 1, 97, 700], seed=12), kernel=kern)
 
 
-def test_pipe_paths_fallback_rows_match_oracle():
+@pipes
+def test_pipe_paths_fallback_rows_match_oracle(kern):
     """Models whose feeder row takes its light term: those rows run on the chain kernel's path
     variant and its traceback, the others on the pipelined plan; every path equals the oracle's."""
     total_fb = 0
     for seed in range(6):
-        hmm = random_chain_hmm(300, S=8, seed=seed)
+        hmm = random_chain_hmm(300 if kern == _lib.SVH_KERNEL_PIPE else 700, S=8, seed=seed)
         rows, cols = hmm.trans_rows.astype(np.int64), hmm.trans_cols.astype(np.int64)
         probs = hmm.trans_probs.copy()
         probs[(cols == 0) & (rows != 0)] = np.float32(0.0)
         hmm.trans_probs = probs
-        total_fb += decode_check(hmm, random_seqs(8, [700, 1, 40, 333], seed=seed))
+        total_fb += decode_check(hmm, random_seqs(8, [700, 1, 40, 333], seed=seed), kernel=kern)
     assert total_fb > 0
 
 
+@pipes
 @pytest.mark.parametrize("name", ["100.chmm", "1001.chmm", "2050.chmm"])
-def test_pipe_paths_reference_models_vs_oracle(name):
+def test_pipe_paths_reference_models_vs_oracle(name, kern):
     hmm = svh.read_HMM(chmm(name))
     seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))[:3]
-    assert decode_check(hmm, seqs) == 0
+    assert decode_check(hmm, seqs, kernel=kern) == 0
 
 
-def test_pipe_paths_covid_entries_through_match_states():
+@pipes
+def test_pipe_paths_covid_entries_through_match_states(kern):
     """covid-19 sequences whose best paths run N -> match states -> C (the j* recompute at the
     entry into C) on 2405.chmm, against the oracle's decode."""
     hmm = svh.read_HMM(chmm("2405.chmm"))
     seqs = svh.read_emit_seq(ess("covid-19.ess"))
     short = [s for s in seqs if len(s) < 1500][:4]
-    assert decode_check(hmm, short) == 0
+    assert decode_check(hmm, short, kernel=kern) == 0
+
+
+@pytest.mark.parametrize("copies", [2, 8])
+def test_pipew_paths_replicated_headline_digests(copies):
+    """Wide path batches (AUTO past the latency plan's range: 100 and 400 sequences of
+    2405.chmm x emit_50_3500_20, 2 and 8 sequences per workgroup): every row's scores, best state
+    and path against the committed oracle digests, no fallback row."""
+    import hashlib
+    import json
+    import os
+    from tests.conftest import ROOT
+
+    rows = json.load(open(os.path.join(ROOT, "tests", "golden", "score_digests.json")))[
+        "2405.chmm x emit_50_3500_20.ess"]
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess")) * copies
+    model = svh.DeviceModel(hmm)
+    batch = model.batch(seqs, paths=True)
+    plan = batch.plan()
+    assert plan["kernel"] == _lib.SVH_KERNEL_PIPE_WIDE, plan
+    batch.run()
+    s, b, pth = batch.read(want_paths=True)
+    assert batch.fallbacks() == 0
+    for q in range(len(seqs)):
+        r = rows[q % 50]
+        assert hashlib.sha256(np.ascontiguousarray(s[q]).tobytes()).hexdigest() == r["scores_sha256"], q
+        assert b[q] == r["best_state"], q
+        assert hashlib.sha256(np.asarray(pth[q], np.int32).tobytes()).hexdigest() == r["path_sha256"], q
+    batch.close()
+    model.close()
