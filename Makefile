@@ -52,7 +52,8 @@ PIPE_OBJS := pipe pipe_tm1 pipe_tm1p
 $(BUILD)/pipe.hazards: $(foreach o,$(PIPE_OBJS),$(BUILD)/$(o).o) tools/dpp_hazards.py
 	set -e; for o in $(PIPE_OBJS); do \
 	  (cd $(BUILD) && /opt/rocm/lib/llvm/bin/llvm-objdump --offloading $$o.o > /dev/null); \
-	  /opt/rocm/lib/llvm/bin/llvm-objdump -d $(BUILD)/$$o.o.0.hipv4-amdgcn-amd-amdhsa--gfx950 > $(BUILD)/$$o.s; \
+	  co=$(BUILD)/$$o.o.0.hipv4-amdgcn-amd-amdhsa--gfx950; [ -f $$co ] || continue; \
+	  /opt/rocm/lib/llvm/bin/llvm-objdump -d $$co > $(BUILD)/$$o.s; \
 	  python3 tools/dpp_hazards.py $(BUILD)/$$o.s pipe_viterbi_kernel; done > $@
 
 # Oracle: plain C, every add rounded on its own (test infrastructure only).

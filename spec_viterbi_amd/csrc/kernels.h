@@ -221,7 +221,7 @@ struct PipeModel {
     uint32_t diag;               // diagnostics with stamps (SVH_PIPE_DEBUG bits > 1): 1 = no boundary
                                  // exchange (every wave runs as block 0; timing only, wrong results)
 };
-constexpr int kPipeStamps = 12;  // written only by -DSVH_PIPE_DIAG builds of pipe.hip
+constexpr int kPipeStamps = 13;  // written only by -DSVH_PIPE_DIAG builds of pipe.hip
 // Per-batch scratch of the pipelined kernel (sized for `rows` rows).
 struct PipeScratch {
     uint32_t* ctr;    // [4]: [0] workgroup ticket, [1] finished workgroups, [2] last epoch

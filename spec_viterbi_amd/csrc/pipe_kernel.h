@@ -64,9 +64,10 @@ constexpr uint32_t kGst = SVH_PIPE_GST;
 static_assert(kGpf == 1 || kGpf == 2 || kGpf == 4, "granule prefetch depth");
 static_assert(kGst < 8, "granule store step");
 
-// LDS boundary ring layout (A/B knob): 0 = [u][lane] (every step stores its row, one ds_write_b32);
-// 1 = [u / 8][lane][u % 8]: a group's 8 last-slot scores stay in registers and go out as two
-// ds_write_b128 per group (the consumer reads lane 63's 8 values as one contiguous 32 bytes).
+// LDS boundary ring layout: 0 = [u][lane] (every step stores its row, one ds_write_b32; TM = 0,
+// pipe.hip); 1 = [u / 8][lane][u % 8]: a group's 8 last-slot scores stay in registers and go out as
+// two ds_write_b128 per group (the consumer reads lane 63's 8 values as one contiguous 32 bytes;
+// TM = 1 / 2, pipe_tm1.hip and pipe_tm1p.hip define it).
 #ifndef SVH_PIPE_RING8
 #define SVH_PIPE_RING8 0
 #endif
@@ -176,13 +177,44 @@ __device__ __forceinline__ void chain_terms_v(float& xb, float& xa, float eb, fl
     }
 }
 
+// TM 3: both feeder terms in one packed add, xa = {ea_0 + F, ea_1 + F} (F = the high half of cf),
+// then slot 0's chain term as chain_terms / chain_terms_v (the packed add and, R < 1, the plain add
+// give the DPP read of x its two wait states inside the block).
+template <int R>
+__device__ __forceinline__ void chain_terms_pk(float& xb, f2& xa, f2 ea, float eb, float bnd, f2 cf, float x) {
+    if constexpr (R < 0) {
+        asm("v_pk_add_f32 %1, %3, %5 op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+            "v_add_f32_e32 %0, %2, %4\n\t"
+            "v_add_f32_dpp %0, %6, %4 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb), "=&v"(xa)
+            : "s"(bnd), "v"(ea), "v"(eb), "v"(cf), "v"(x));
+    } else if constexpr (R == 0) {
+        asm("v_pk_add_f32 %1, %3, %5 op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+            "v_add_f32_e32 %0, %2, %4\n\t"
+            "v_add_f32_dpp %0, %6, %4 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb), "=&v"(xa)
+            : "v"(bnd), "v"(ea), "v"(eb), "v"(cf), "v"(x));
+    } else {
+        asm("v_pk_add_f32 %1, %3, %5 op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+            "v_add_f32_dpp %0, %2, %4 row_ror:%7 row_mask:0xf bank_mask:0xf\n\t"
+            "v_add_f32_dpp %0, %6, %4 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb), "=&v"(xa)
+            : "v"(bnd), "v"(ea), "v"(eb), "v"(cf), "v"(x), "n"(16 - R));  // lane 0 <- lane R
+    }
+}
+
 // Table reads of a step (template TM):
 //   0  per-slot tables f32x32 [SM][eb|ea] (symbol o in register o): the compiler's indexed moves,
 //      one s_set_gpr_idx block of SM x 2 v_mov, and the heavy constants by four v_readlane;
 //   1  (SM = 2, at most kPairSym symbols) four pair-interleaved tables pinned to v2..v161,
 //      register 2o + u = value u of symbol o: T1 = {eb_0, ea_0}, T2 = {eb_1, ea_1},
 //      T3 = {A_S, A_F}, T4 = {X_SS, X_FF}; one idx block of four v_mov_b64 (M0 = 2o, the symbol
-//      windows are loaded pre-doubled), so no v_readlane and no SGPR hand-off per step.
+//      windows are loaded pre-doubled), so no v_readlane and no SGPR hand-off per step;
+//   2  the same tables read as M0-indexed operands of the adds that use them (one gpr_idx(SRC0)
+//      block, only eb_0 moved out for slot 0's DPP chain add);
+//   3  as 1 with T1 = {ea_0, ea_1}, T2 = {eb_0, eb_1}: both feeder terms come out of one
+//      v_pk_add_f32 with F broadcast from the high half of the {C, F} pair (op_sel), one VALU less;
+//   4  as 2 with the layout of 3 (the packed feeder add reads T1 as an indexed 64-bit operand).
 // tools/ubench/step_ubench.hip prices the two at 158 vs 101 shader cycles per observation (no
 // exchange, 4 waves per CU).  Measured and not kept (round 3): every table and constant read as an
 // M0-indexed operand of the add that uses it (13 VALU, 66 vs 72 ns a step, 1 % in the pipeline);
@@ -203,7 +235,7 @@ struct ChainIn {
 template <int SM, int W, bool SX, int PATHS, int TM>
 __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     static_assert(TM == 0 || SM == 2, "pair tables: two slots per lane");
-    static_assert(TM >= 0 && TM <= 2, "table mode");
+    static_assert(TM >= 0 && TM <= 4, "table mode");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* ring = lds;                                                  // [W][kR][64]
     uint32_t* cnt = reinterpret_cast<uint32_t*>(ring + W * kR * 64);    // [16]
@@ -248,7 +280,8 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     // diagnostics: 0 loop cycles, 1 head cycles, 2 tail cycles, 3 slow re-reads waiting for the
     // previous wave, 4 ... for the next wave (flow control), 5 ... for granules, 6 ... for the
     // consumer's progress word, 7 body iterations, 8 .. 11 the 100 MHz real-time clock at wave
-    // entry, sweep start, body end, sweep end.  Built only with -DSVH_PIPE_DIAG (tools/ab_build.sh;
+    // entry, sweep start, body end, sweep end, 12 the wave's XCC_ID << 32 | HW_ID (placement).
+    // Built only with -DSVH_PIPE_DIAG (tools/ab_build.sh;
     // then SVH_PIPE_DEBUG=1 at run time): the counters would otherwise hold SGPRs through the loop
     // in the production kernel, whose SGPRs are its scarcest register file.
     unsigned long long dg[kPipeStamps] = {};
@@ -260,6 +293,11 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 #define SVH_RT(k) ((void)0)
 #endif
     SVH_RT(8);
+#ifdef SVH_PIPE_DIAG
+    if (dbg)  // hwreg(HW_REG_XCC_ID) and hwreg(HW_REG_HW_ID), 32 bits each
+        dg[12] = ((unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                 (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
 
     if (act) {
         const uint32_t p0 = blk * 64 * SM + lane * SM;
@@ -278,7 +316,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             }
         // mode 3: the pair-interleaved tables (symbols >= S: +inf)
         constexpr bool kT3 = TM >= 1;  // pair tables (symbols pre-doubled)
-        constexpr bool kT4 = TM == 1;  // ... read by four 64-bit moves
+        constexpr bool kT4 = TM == 1 || TM == 3;  // ... read by four 64-bit moves
         f32x32 TA[4];
         f32x8 TB[4];
         if constexpr (kT3) {
@@ -289,7 +327,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 const float2 e0 = m.tab[((size_t)(blk * S + oc) * SM + 0) * 64 + lane];
                 const float2 e1 = m.tab[((size_t)(blk * S + oc) * SM + 1) * 64 + lane];
                 const float4 h = *reinterpret_cast<const float4*>(m.hc + oc * 8);
-                const float val[4][2] = {{ok ? e0.x : kInf, ok ? e0.y : kInf}, {ok ? e1.x : kInf, ok ? e1.y : kInf},
+                // TM 3: {ea_0, ea_1}, {eb_0, eb_1}; otherwise {eb_0, ea_0}, {eb_1, ea_1}
+                const float2 t1 = TM >= 3 ? make_float2(e0.y, e1.y) : e0, t2 = TM >= 3 ? make_float2(e0.x, e1.x) : e1;
+                const float val[4][2] = {{ok ? t1.x : kInf, ok ? t1.y : kInf}, {ok ? t2.x : kInf, ok ? t2.y : kInf},
                                          {ok ? h.x : kInf, ok ? h.y : kInf}, {ok ? h.z : kInf, ok ? h.w : kInf}};
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
@@ -469,7 +509,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         auto step = [&](uint32_t o, auto in) {
             constexpr int R = decltype(in)::value;
             float xa[SM], xb[SM];  // feeder and chain terms of every slot
-            if constexpr (TM == 2) {  // o is 2 x the symbol: the table reads are indexed operands
+            if constexpr (TM == 2 || TM == 4) {  // o is 2 x the symbol: the table reads are indexed operands
                 // of the adds that use them (one gpr_idx(SRC0) block; only eb_0 is moved out, for
                 // slot 0's DPP chain add)
                 const float pm = fminf(v[0], v[1]);  // the heavy side reads the scores of t-1
@@ -480,6 +520,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 #pragma clang diagnostic ignored "-Wuninitialized"
+                if constexpr (TM == 2) {
                 asm("s_set_gpr_idx_on %[o], gpr_idx(SRC0)\n\t"
                     "v_mov_b32 %[eb0], v2\n\t"
                     "v_add_f32 %[xa0], v3, %[f]\n\t"
@@ -494,6 +535,23 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                       "{v[34:41]}"(TB[0]), "{v[42:73]}"(TA[1]), "{v[74:81]}"(TB[1]), "{v[82:113]}"(TA[2]),
                       "{v[114:121]}"(TB[2]), "{v[122:153]}"(TA[3]), "{v[154:161]}"(TB[3])
                     : "m0");
+                } else {  // T1 = {ea_0, ea_1}: one packed feeder add, F from the high half of CF
+                f2 xap;
+                asm("s_set_gpr_idx_on %[o], gpr_idx(SRC0)\n\t"
+                    "v_mov_b32 %[eb0], v42\n\t"
+                    "v_pk_add_f32 %[xa], v[2:3], %[cf] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+                    "v_add_f32 %[xb1], v43, %[v0]\n\t"
+                    "v_pk_add_f32 %[s1], v[82:83], %[pm] op_sel_hi:[1,0]\n\t"
+                    "v_pk_add_f32 %[s2], v[122:123], %[cf]\n\t"
+                    "s_set_gpr_idx_off"
+                    : [eb0] "=&v"(eb0), [xa] "=&v"(xap), [xb1] "=&v"(xb[1]), [s1] "=&v"(s1), [s2] "=&v"(s2)
+                    : [o] "s"(o), [v0] "v"(v[0]), [pm] "v"(pmv), [cf] "v"(CF), "{v[2:33]}"(TA[0]),
+                      "{v[34:41]}"(TB[0]), "{v[42:73]}"(TA[1]), "{v[74:81]}"(TB[1]), "{v[82:113]}"(TA[2]),
+                      "{v[114:121]}"(TB[2]), "{v[122:153]}"(TA[3]), "{v[154:161]}"(TB[3])
+                    : "m0");
+                xa[0] = xap.x;
+                xa[1] = xap.y;
+                }
 #pragma clang diagnostic pop
                 xb[0] = chain_b<R>(eb0, in.b, v[1]);
                 float cn = fminf(s1.x, s2.x);
@@ -530,10 +588,18 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                       "{v[82:113]}"(TA[2]), "{v[114:121]}"(TB[2]), "{v[122:153]}"(TA[3]), "{v[154:161]}"(TB[3])
                     : "m0");
 #pragma clang diagnostic pop
-                if constexpr (R < 0) chain_terms(xb[0], xa[0], p0.x, p0.y, in.b, CF.y, v[1]);
-                else chain_terms_v<R>(xb[0], xa[0], p0.x, p0.y, in.b, CF.y, v[1]);
-                xa[1] = p1.y + CF.y;
-                xb[1] = p1.x + v[0];
+                if constexpr (TM == 3) {  // p0 = {ea_0, ea_1}, p1 = {eb_0, eb_1}
+                    f2 xap;
+                    chain_terms_pk<R>(xb[0], xap, p0, p1.x, in.b, CF, v[1]);
+                    xa[0] = xap.x;
+                    xa[1] = xap.y;
+                    xb[1] = p1.y + v[0];
+                } else {
+                    if constexpr (R < 0) chain_terms(xb[0], xa[0], p0.x, p0.y, in.b, CF.y, v[1]);
+                    else chain_terms_v<R>(xb[0], xa[0], p0.x, p0.y, in.b, CF.y, v[1]);
+                    xa[1] = p1.y + CF.y;
+                    xb[1] = p1.x + v[0];
+                }
                 const float pm = fminf(v[0], v[1]);
                 const f2 s1 = kS + (f2){pm, pm};  // A_S + m, A_F + m
                 const f2 s2 = kX + CF;            // X_SS + c, X_FF + F

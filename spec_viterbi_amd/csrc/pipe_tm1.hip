@@ -1,20 +1,35 @@
 // Pipelined chain Viterbi kernel, TM = 1 (pair tables read by 64-bit moves; pipe_kernel.h):
 // scores-only instantiations, 2 slots per lane, 4 waves per workgroup (one per SIMD: the 258
 // registers of the pair tables do not fit the 256 of two waves per SIMD, which spilled).
+// The LDS boundary ring of these instantiations is batched per group of 8 (SVH_PIPE_RING8 = 1: two
+// ds_write_b128 per group instead of a ds_write_b32 per step).  With the pair-table step the
+// per-step LDS store paced the pipeline: 0.363 -> 0.282 ms on the headline (profiles/r04_s4/ab.log;
+// TM = 0 in pipe.hip keeps the per-step row, 0.335 vs 0.342 ms batched).
+#ifndef SVH_PIPE_RING8
+#define SVH_PIPE_RING8 1
+#endif
 #include "pipe_kernel.h"
 
 namespace svh {
 
 const void* pipe_kernel_tm1(int sm, int waves, bool sx, int paths) {
-    if (sm != 2 || (paths && paths != -2)) return nullptr;
+    if (sm != 2 || (paths && (paths < -4 || paths > -2))) return nullptr;
 #ifdef SVH_PIPE_AB_ONLY  // A/B timing builds: the headline geometry only
     if (paths == -2) return waves == 4 && !sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 2>) : nullptr;
+    if (paths == -3) return waves == 4 && !sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 3>) : nullptr;
+    if (paths == -4) return waves == 4 && !sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 4>) : nullptr;
     return waves == 4 && !sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 1>) : nullptr;
 #else
     if (waves != 4) return nullptr;
     if (paths == -2)  // TM = 2 (indexed operands; A/B: SVH_PIPE_TM=2)
         return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 2>)
                   : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 2>);
+    if (paths == -3)  // TM = 3 (packed feeder terms; A/B: SVH_PIPE_TM=3)
+        return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 3>)
+                  : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 3>);
+    if (paths == -4)  // TM = 4 (indexed operands, packed feeder terms; A/B: SVH_PIPE_TM=4)
+        return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 4>)
+                  : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 4>);
     return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 1>)
               : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 1>);
 #endif

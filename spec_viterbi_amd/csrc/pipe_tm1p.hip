@@ -1,5 +1,12 @@
 // Pipelined chain Viterbi kernel, TM = 1 (pair tables read by 64-bit moves; pipe_kernel.h):
 // decoded-path instantiations (PATHS 1 and 2), 2 slots per lane, 4 waves per workgroup.
+// The LDS boundary ring of these instantiations is batched per group of 8 (SVH_PIPE_RING8 = 1: two
+// ds_write_b128 per group instead of a ds_write_b32 per step).  With the pair-table step the
+// per-step LDS store paced the pipeline: 0.363 -> 0.282 ms on the headline (profiles/r04_s4/ab.log;
+// TM = 0 in pipe.hip keeps the per-step row, 0.335 vs 0.342 ms batched).
+#ifndef SVH_PIPE_RING8
+#define SVH_PIPE_RING8 1
+#endif
 #include "pipe_kernel.h"
 
 namespace svh {

@@ -3,6 +3,7 @@
 #include "runtime.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -782,9 +783,9 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     // per-slot tables (A/B and tests)
     view.wide = p.wide ? 1u : 0u;
     view.tm = !p.wide && p.SM == 2 && p.W == 4 && S <= kPairSymbols ? 1u : 0u;
-    if (const char* e = std::getenv("SVH_PIPE_TM"); e) {  // A/B: 0 per-slot tables, 2 indexed operands
-        const int t = std::atoi(e);
-        if (t == 0 || (t == 2 && view.tm)) view.tm = (uint32_t)t;
+    if (const char* e = std::getenv("SVH_PIPE_TM"); e) {  // A/B: 0 per-slot tables, 2 indexed operands,
+        const int t = std::atoi(e);                           // 3 packed feeder terms, 4 both
+        if (t == 0 || (t >= 2 && t <= 4 && view.tm)) view.tm = (uint32_t)t;
     }
     if (const char* e = std::getenv("SVH_PIPE_DEBUG"); e && std::atoi(e)) {  // diagnostics only
         d_stamps.alloc((size_t)65536 * kPipeStamps * 8);
@@ -830,7 +831,10 @@ void DevicePipePlan::report_stamps(uint32_t nseq) const {
                     if (w == 0) st = r[9] - t0;
                     ed = std::max(ed, r[11] - t0);
                 }
-                std::fprintf(stderr, " [g%u in %.1f st %.1f end %.1f]", g, en * 0.01, st * 0.01, ed * 0.01);
+                // placement of the workgroup's first wave: XCC and CU (HW_ID bits 11:8) / SE (14:13)
+                const unsigned long long hw = h[(((size_t)q * plan.G + g) * plan.W) * kPipeStamps + 12];
+                std::fprintf(stderr, " [g%u in %.1f st %.1f end %.1f x%u s%u c%u]", g, en * 0.01, st * 0.01, ed * 0.01,
+                             (unsigned)(hw >> 32) & 0xFu, (unsigned)(hw >> 13) & 0x3u, (unsigned)(hw >> 8) & 0xFu);
             }
             std::fprintf(stderr, "\n");
         }
@@ -1319,6 +1323,8 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
                   s_pm = section(pp ? (size_t)nseq * 8 : 0), s_pr = section(pp ? (size_t)nseq * 8 : 0),
                   s_pc = section(pp ? (size_t)nseq * 8 : 0), s_fc = section(pp ? (size_t)nseq * 8 : 0),
                   s_bp = section(fp ? (size_t)nseq * 8 : 0);
+    static const bool trace = std::getenv("SVH_TRACE_ONESHOT") && std::atoi(std::getenv("SVH_TRACE_ONESHOT"));
+    const auto tl0 = std::chrono::steady_clock::now();
     uint8_t* const hin = h_in.reserve(in_bytes);
     const uint64_t S = model->host.S;
     for (uint32_t q = 0; q < nseq; ++q) {
@@ -1373,8 +1379,15 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
     put(s_pc, h_pcoff.data());
     put(s_fc, h_fcoff.data());
     put(s_bp, h_bpoff.data());
+    const auto tl1 = std::chrono::steady_clock::now();
     d_in.reserve(in_bytes);
     hip_check(hipMemcpyAsync(d_in.ptr, hin, in_bytes, hipMemcpyHostToDevice, s), "batch inputs H2D");
+    if (trace) {
+        const auto tl2 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "load trace (us): pack %.1f h2d-enqueue %.1f (%zu bytes)\n",
+                     std::chrono::duration<double, std::micro>(tl1 - tl0).count(),
+                     std::chrono::duration<double, std::micro>(tl2 - tl1).count(), in_bytes);
+    }
     uint8_t* const din = d_in.as<uint8_t>();
     p_sym = din + s_sym.off;
     p_symoff = reinterpret_cast<uint64_t*>(din + s_symoff.off);

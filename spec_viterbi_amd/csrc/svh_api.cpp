@@ -1,5 +1,8 @@
 // extern "C" boundary (include/svh.h).  Every entry point catches everything, records a
 // thread-local message and returns a status code: no exception crosses the ABI.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <memory>
 #include <mutex>
@@ -301,9 +304,33 @@ void oneshot(svh_model_t m, uint32_t level, uint64_t nseq, const uint64_t* offse
         static const uint8_t zero = 0;
         b = std::make_unique<svh::Batch>(m->impl.get(), 1, one, &zero, paths ? SVH_BATCH_PATHS : 0u);
     }
+    // SVH_TRACE_ONESHOT=1 (diagnostics): host microseconds of each phase and the GPU time from the
+    // call's first enqueue to the run's start event, on stderr
+    static const bool trace = std::getenv("SVH_TRACE_ONESHOT") && std::atoi(std::getenv("SVH_TRACE_ONESHOT"));
+    if (!trace) {
+        b->load(nseq, offsets, sym64, sym8, m->impl->stream, seqp);
+        b->run(level, nullptr);
+        b->read(nullptr, scores, best_state, paths);
+        return;
+    }
+    using clk = std::chrono::steady_clock;
+    hipEvent_t e0;
+    (void)hipEventCreate(&e0);
+    const auto t0 = clk::now();
+    (void)hipEventRecord(e0, m->impl->stream);
     b->load(nseq, offsets, sym64, sym8, m->impl->stream, seqp);
+    const auto t1 = clk::now();
     b->run(level, nullptr);
+    const auto t2 = clk::now();
     b->read(nullptr, scores, best_state, paths);
+    const auto t3 = clk::now();
+    float upload_ms = 0.0f, kernel_ms = 0.0f;
+    (void)hipEventElapsedTime(&upload_ms, e0, b->ev_start);
+    (void)hipEventElapsedTime(&kernel_ms, b->ev_start, b->ev_stop);
+    (void)hipEventDestroy(e0);
+    auto us = [](clk::time_point a, clk::time_point c) { return std::chrono::duration<double, std::micro>(c - a).count(); };
+    std::fprintf(stderr, "oneshot trace (us): load %.1f run-enqueue %.1f read %.1f total %.1f | gpu: upload-to-run-start %.1f "
+                 "run %.1f\n", us(t0, t1), us(t1, t2), us(t2, t3), us(t0, t3), upload_ms * 1e3, kernel_ms * 1e3);
 }
 }  // namespace
 

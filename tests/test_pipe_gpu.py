@@ -15,7 +15,8 @@ import spec_viterbi_amd as svh
 from spec_viterbi_amd import _lib
 from oracle import oracle
 from tests.conftest import chmm, ess
-from tests.helpers import bit_equal, first_mismatch, from_hex, load_golden, random_chain_hmm, random_seqs
+from tests.helpers import (bit_equal, first_mismatch, from_hex, load_digests, load_golden, random_chain_hmm,
+                           random_seqs)
 
 pytestmark = pytest.mark.gpu
 PIPES = [_lib.SVH_KERNEL_PIPE, _lib.SVH_KERNEL_PIPE_WIDE]
@@ -205,6 +206,31 @@ def test_pipe_geometries(geom, monkeypatch):
     assert (plan["slots"], plan["pipe_waves"]) == geom
     assert fb == 0
     oracle_check(hmm, seqs, s, b)
+
+
+@pytest.mark.parametrize("tm", [0, 1, 2, 3, 4])
+def test_pipe_table_modes(tm, monkeypatch):
+    """Every step table mode of the latency plan (pipe_kernel.h TM: per-slot tables, pair tables by
+    64-bit moves, indexed operands, packed feeder terms, both) on the headline rows against the
+    goldens and on random chain models (ties, +inf edges, light starts, chain breaks, lengths around
+    the group / window boundaries) against the oracle."""
+    monkeypatch.setenv("SVH_PIPE_TM", str(tm))
+    import hashlib
+
+    rows = load_digests()["2405.chmm x emit_50_3500_20.ess"]
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
+    s, b, fb, plan = run(hmm, seqs)
+    assert plan["kernel"] == _lib.SVH_KERNEL_PIPE and fb == 0
+    for q in range(len(seqs)):
+        assert hashlib.sha256(np.ascontiguousarray(s[q]).tobytes()).hexdigest() == rows[q]["scores_sha256"], q
+        assert b[q] == rows[q]["best_state"], q
+    for k, kw in enumerate([dict(n_from_m=False), dict(ties=True), dict(inf_edges=0.1), dict(start=(0, 5, 301)),
+                            dict(gap=37), dict(self_c=False)]):
+        hmm = random_chain_hmm(1300, S=20, seed=40 + k, **kw)
+        seqs = random_seqs(20, [1, 7, 8, 9, 33, 500, 1025, 2100], seed=50 + k)
+        s, b, fb, plan = run(hmm, seqs)
+        oracle_check(hmm, seqs, s, b)
 
 
 @pipes
