@@ -504,15 +504,25 @@ def main(argv=None):
     value = total_updates * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
 
-    # host-to-host (svh_viterbi: symbols H2D, run, scores D2H), rank 0 only, after the timed region
-    e2e_ms = None
+    # host-to-host, rank 0 only, after the timed region: symbols in the device format (packed uint8,
+    # what svh_reader_next yields; svh_viterbi_u8: H2D, run, D2H of scores and best states), and
+    # from the reader's list of uint64 arrays (svh_viterbi_seqs, narrowed on the host per call)
+    e2e_ms = e2e_list_ms = None
     if rank == 0 and seqs and not strong:
-        e2e = []
-        for _ in range(5):
-            t_e = time.perf_counter()
-            model.viterbi(seqs, level=args.level)
-            e2e.append(time.perf_counter() - t_e)
-        e2e_ms = float(np.median(e2e)) * 1e3
+        from spec_viterbi_amd.hmm import pack_sequences
+        offs, sym64 = pack_sequences(seqs)
+        sym8 = sym64.astype(np.uint8)
+
+        def med(f):
+            f()
+            ts = []
+            for _ in range(9):
+                t_e = time.perf_counter()
+                f()
+                ts.append(time.perf_counter() - t_e)
+            return float(np.median(ts)) * 1e3
+        e2e_ms = med(lambda: model.viterbi_packed(offs, sym8, level=args.level))
+        e2e_list_ms = med(lambda: model.viterbi(seqs, level=args.level))
 
     if rank == 0:
         nnz = int(info["nnz"])
@@ -564,13 +574,17 @@ def main(argv=None):
                 "kernel_ms": round(kernel_ms, 4),
                 "setup_ms": round(float(np.median(setup)) * 1e3, 3),
                 "e2e_ms_per_step": None if e2e_ms is None else round(e2e_ms, 3),
+                "e2e_over_kernel_ms": None if e2e_ms is None else round(e2e_ms - kernel_ms, 3),
+                "e2e_list_u64_ms_per_step": None if e2e_list_ms is None else round(e2e_list_ms, 3),
                 "e2e_M_state_updates_per_s": None if not e2e_ms else round(updates_per_rank / e2e_ms / 1e3, 2),
                 "setup_plus_e2e_M_state_updates_per_s": None if not e2e_ms else
                 round(updates_per_rank / (e2e_ms + float(np.median(setup)) * 1e3) / 1e3, 2),
                 "gather_ms": round(gather_ms, 3) if gather_ms is not None else None,
                 "note": "setup_ms = svh_model_create (host CSR + plans + upload; the reference rebuilds its model inside "
-                        "every run_Viterbi call, bench_Viterbi.h:53-56); e2e = svh_viterbi host symbols -> host scores "
-                        "(batch upload, run, D2H), median of 5 on rank 0",
+                        "every run_Viterbi call, bench_Viterbi.h:53-56); e2e = svh_viterbi_u8 from host symbols in the device "
+                        "format (packed uint8, as svh_reader_next yields them) to host scores and best states (batch "
+                        "upload, run, D2H), median of 9 on rank 0; e2e_list_u64 = the same from the reader's list of "
+                        "uint64 arrays (svh_viterbi_seqs, narrowed per call)",
             },
             "roofline": rl,
         }

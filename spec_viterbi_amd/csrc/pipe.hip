@@ -44,7 +44,7 @@ hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratc
     // TM = 1 (pair tables) needs 2 slots per lane and at most kPairSym symbols
     if (m.tm && (m.SM != 2 || m.S > kPairSym)) return hipErrorInvalidValue;
     const void* fn = !m.tm ? pipe_kernel_tm0((int)m.SM, (int)m.W, m.sx != 0, pv)
-                     : paths ? pipe_kernel_tm1_paths((int)m.SM, (int)m.W, m.sx != 0, pv)
+                     : paths ? pipe_kernel_tm1_paths((int)m.SM, (int)m.W, m.sx != 0, pv, m.tm == 4 ? 4 : 1)
                              : pipe_kernel_tm1((int)m.SM, (int)m.W, m.sx != 0, m.tm >= 2 ? -(int)m.tm : 0);
     if (!fn || m.S > 32 || m.G == 0 || m.nblk > m.G * m.W || m.P != m.nblk * 64 * m.SM || !x.ctr ||
         b.nseq > x.rows || x.G < m.G)

@@ -82,6 +82,16 @@ __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// LDS reads of the exchange kept where they are issued (A/B knob SVH_PIPE_LDSX, default 1): the
+// compiler otherwise (a) hoisted the slow path's re-load of the next group's boundary vector out of
+// its branch, so every group re-read it at its first use and waited for it there, and (b) moved the
+// readfirstlane of the neighbours' counts (read four steps before their use) up to the reads,
+// waiting for them at once.  An opaque zero in the slow path's address and an asm use of each count
+// where it is needed keep both reads' latency behind steps.
+#ifndef SVH_PIPE_LDSX
+#define SVH_PIPE_LDSX 1
+#endif
+
 // The granule consumer's progress store (once per 32 observations, after the prefetch of the last
 // group) is a vector-memory operation too: the next iteration's first two groups have it queued
 // after their own prefetch, so they wait for one operation more than kGpf - 1, or the in-order
@@ -880,6 +890,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             g_prefetch64(gq[j % kGpf], gin + ((tg + 8 * kGpf + (lane & 7u)) & (kGR - 1)));
                         }
                         if constexpr (DST == 1) {
+                            if constexpr (SVH_PIPE_LDSX) asm volatile("" : "+v"(nc_rd));
                             if ((int)uniform((int)nc_rd) < (int)tg + 8 - (int)kR) wait_next((int)tg + 8 - (int)kR);
                         }
                         auto one = [&](auto kc) {
@@ -889,7 +900,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                 if (!next_ok) {  // the producer had not published this group: wait, re-load
                                     wait_prev(tg + 8);
                                     asm volatile("" ::: "memory");
-                                    bv_next = ring_prev[ring_idx(8 * j + (lane & 7u), 63)];
+                                    uint32_t z = 0;  // SVH_PIPE_LDSX: an address the compiler cannot hoist
+                                    if constexpr (SVH_PIPE_LDSX) asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                                    bv_next = ring_prev[ring_idx(8 * j + (lane & 7u), 63) + z];
                                 }
                             }
                             if constexpr (SRC == 1) bv = bv_next;
@@ -913,7 +926,11 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                 asm volatile("" ::: "memory");
                                 if constexpr (SRC == 1) pc_rd = lds_ld32(cnt_w - 1);
                                 if constexpr (DST == 1) nc_rd = lds_ld32(cnt_w + 1);
+                                // SVH_PIPE_LDSX: issued here, not where the scheduler would sink them (the
+                                // group's end, right before their use)
+                                if constexpr (SVH_PIPE_LDSX) __builtin_amdgcn_sched_barrier(0);
                             }
+                            if constexpr (SVH_PIPE_LDSX && SVH_PIPE_RING8 && k == 3) __builtin_amdgcn_sched_barrier(0);
                             if constexpr (DST == 2 && kGst != 0 && k == kGst) {  // the last group's granules
                                 if (gpend_t && lane < 8)
                                     g_st64(gout + ((gpend_t + lane) & (kGR - 1)),
@@ -933,6 +950,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         asm volatile("" ::: "memory");
                         put_cnt(tg + 8);
                         if constexpr (SRC == 1) {  // the next group's boundary vector (valid if next_ok)
+                            if constexpr (SVH_PIPE_LDSX) asm volatile("" : "+v"(pc_rd));
                             next_ok = (uint32_t)uniform((int)pc_rd) >= tg + 16;
                             asm volatile("" ::: "memory");
                             bv_next = ring_prev[ring_idx(((8 * j + 8) & (kR - 1)) + (lane & 7u), 63)];
@@ -1097,11 +1115,11 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 }  // namespace
 
 // The kernel's instantiations live in three translation units (they compile in parallel):
-// pipe.hip TM = 0 (every geometry, decoded-path variants at 2 x 4), pipe_tm1.hip TM = 1 (2 slots,
-// 4 waves), pipe_tm1p.hip TM = 1 decoded-path variants (2 x 4).  Each returns the kernel for
+// pipe.hip TM = 0 (every geometry, decoded-path variants at 2 x 4), pipe_tm1.hip TM = 1..4 (2 slots,
+// 4 waves), pipe_tm1p.hip TM = 1 / 4 decoded-path variants (2 x 4).  Each returns the kernel for
 // (slots, waves, sx, PATHS, ties_heavy) or nullptr.
 const void* pipe_kernel_tm0(int sm, int waves, bool sx, int paths);
 const void* pipe_kernel_tm1(int sm, int waves, bool sx, int paths);
-const void* pipe_kernel_tm1_paths(int sm, int waves, bool sx, int paths);
+const void* pipe_kernel_tm1_paths(int sm, int waves, bool sx, int paths, int tm);
 
 }  // namespace svh

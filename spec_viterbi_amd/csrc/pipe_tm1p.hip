@@ -1,4 +1,4 @@
-// Pipelined chain Viterbi kernel, TM = 1 (pair tables read by 64-bit moves; pipe_kernel.h):
+// Pipelined chain Viterbi kernel, pair tables (pipe_kernel.h TM = 4, the default, and TM = 1):
 // decoded-path instantiations (PATHS 1 and 2), 2 slots per lane, 4 waves per workgroup.
 // The LDS boundary ring of these instantiations is batched per group of 8 (SVH_PIPE_RING8 = 1: two
 // ds_write_b128 per group instead of a ds_write_b32 per step).  With the pair-table step the
@@ -11,11 +11,18 @@
 
 namespace svh {
 
-const void* pipe_kernel_tm1_paths(int sm, int waves, bool sx, int paths) {
+const void* pipe_kernel_tm1_paths(int sm, int waves, bool sx, int paths, int tm) {
 #ifdef SVH_PIPE_AB_ONLY
     return nullptr;
 #else
     if (sm != 2 || waves != 4 || paths < 1 || paths > 2) return nullptr;
+    if (tm == 4) {  // indexed operands, packed feeder terms
+        if (paths == 2)
+            return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 2, 4>)
+                      : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 2, 4>);
+        return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 1, 4>)
+                  : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 1, 4>);
+    }
     if (paths == 2)
         return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 2, 1>)
                   : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 2, 1>);

@@ -779,13 +779,15 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     view.W = p.W;
     view.G = p.G;
     view.sx = p.sx ? 1u : 0u;
-    // the pair-table step (pipe_kernel.h TM = 1) wherever it applies; SVH_PIPE_TM=0 forces the
-    // per-slot tables (A/B and tests)
     view.wide = p.wide ? 1u : 0u;
-    view.tm = !p.wide && p.SM == 2 && p.W == 4 && S <= kPairSymbols ? 1u : 0u;
-    if (const char* e = std::getenv("SVH_PIPE_TM"); e) {  // A/B: 0 per-slot tables, 2 indexed operands,
-        const int t = std::atoi(e);                           // 3 packed feeder terms, 4 both
-        if (t == 0 || (t >= 2 && t <= 4 && view.tm)) view.tm = (uint32_t)t;
+    // the pair-table step wherever it applies: TM = 4 (indexed operands, packed feeder terms:
+    // 0.255 ms on the headline against 0.263 / 0.268 / 0.277 for TM 2 / 3 / 1 and 0.334 for the
+    // per-slot tables); SVH_PIPE_TM selects another mode (A/B and tests: 0 per-slot
+    // tables, 1 pair tables by 64-bit moves, 2 indexed operands, 3 packed feeder terms, 4 both)
+    view.tm = !p.wide && p.SM == 2 && p.W == 4 && S <= kPairSymbols ? 4u : 0u;
+    if (const char* e = std::getenv("SVH_PIPE_TM"); e) {
+        const int t = std::atoi(e);
+        if (t == 0 || (t >= 1 && t <= 4 && view.tm)) view.tm = (uint32_t)t;
     }
     if (const char* e = std::getenv("SVH_PIPE_DEBUG"); e && std::atoi(e)) {  // diagnostics only
         d_stamps.alloc((size_t)65536 * kPipeStamps * 8);
@@ -832,9 +834,13 @@ void DevicePipePlan::report_stamps(uint32_t nseq) const {
                     ed = std::max(ed, r[11] - t0);
                 }
                 // placement of the workgroup's first wave: XCC and CU (HW_ID bits 11:8) / SE (14:13)
-                const unsigned long long hw = h[(((size_t)q * plan.G + g) * plan.W) * kPipeStamps + 12];
-                std::fprintf(stderr, " [g%u in %.1f st %.1f end %.1f x%u s%u c%u]", g, en * 0.01, st * 0.01, ed * 0.01,
-                             (unsigned)(hw >> 32) & 0xFu, (unsigned)(hw >> 13) & 0x3u, (unsigned)(hw >> 8) & 0xFu);
+                // and its shader clock over the body: s_memtime cycles / s_memrealtime (100 MHz) span
+                const unsigned long long* r0 = h.data() + (((size_t)q * plan.G + g) * plan.W) * kPipeStamps;
+                const unsigned long long hw = r0[12];
+                const double mhz = r0[10] > r0[9] ? (double)r0[0] / ((double)(r0[10] - r0[9]) * 0.01) : 0.0;
+                std::fprintf(stderr, " [g%u in %.1f st %.1f end %.1f x%u s%u c%u %.0fMHz]", g, en * 0.01, st * 0.01,
+                             ed * 0.01, (unsigned)(hw >> 32) & 0xFu, (unsigned)(hw >> 13) & 0x3u,
+                             (unsigned)(hw >> 8) & 0xFu, mhz);
             }
             std::fprintf(stderr, "\n");
         }
@@ -1334,12 +1340,14 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
         // narrow into pinned staging; the range check is a branch-free OR the loop vectorises,
         // the error path re-scans for the offending symbol
         if (sym64 || seqp) {
-            const uint64_t* src = seqp ? seqp[q] : sym64 + base;
+            // (restrict: a uint8_t store may alias anything, which kept the loop byte-serial)
+            const uint64_t* __restrict__ src = seqp ? seqp[q] : sym64 + base;
+            uint8_t* __restrict__ d = dstp;
             uint64_t bad = 0;
             for (uint32_t i = 0; i < L; ++i) {
                 const uint64_t x = src[i];
                 bad |= x >= S ? 1u : 0u;
-                dstp[i] = (uint8_t)x;
+                d[i] = (uint8_t)x;
             }
             if (bad)
                 for (uint32_t i = 0; i < L; ++i)
@@ -1347,13 +1355,13 @@ void Batch::load(uint64_t nseq_, const uint64_t* offs, const uint64_t* sym64, co
                         throw Error(SVH_E_RANGE, "symbol " + std::to_string(src[i]) +
                                                      " out of range (emit_num " + std::to_string(S) + ")");
         } else {
-            const uint8_t* src = sym8 + base;
-            uint32_t bad = 0;
-            for (uint32_t i = 0; i < L; ++i) {
-                const uint32_t x = src[i];
-                bad |= x >= S ? 1u : 0u;
-                dstp[i] = (uint8_t)x;
-            }
+            // the device format already: one memcpy, then a range check the compiler vectorises (a
+            // byte loop that copies and checks ran at ~4 GB/s: 43 us for the headline's 175 KB)
+            const uint8_t* __restrict__ src = sym8 + base;
+            std::memcpy(dstp, src, L);
+            uint8_t mx = 0;
+            for (uint32_t i = 0; i < L; ++i) mx = src[i] > mx ? src[i] : mx;
+            const uint32_t bad = mx >= S ? 1u : 0u;
             if (bad)
                 for (uint32_t i = 0; i < L; ++i)
                     if (src[i] >= S)
@@ -1833,6 +1841,9 @@ void Batch::read(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out
     const size_t pre = sb ? score_off + sb : bb ? best_off + bb : 16;
     const size_t pb = paths_out ? (size_t)total * 4 : 0, path_off = (pre + 15) & ~(size_t)15;
     uint8_t* st = h_out.reserve(path_off + pb);
+    // One copy, one synchronisation, then out to the caller.  (Four pieces with an event each, the
+    // host copying one out while the next moved, were slower: 83 vs 42 us for the headline's 482 KB,
+    // profiles/r04_s8/e2e_split.json.)
     hip_check(hipMemcpyAsync(st, d_out.ptr, pre, hipMemcpyDeviceToHost, s), "results D2H");
     if (pb) hip_check(hipMemcpyAsync(st + path_off, d_paths.ptr, pb, hipMemcpyDeviceToHost, s), "paths D2H");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");

@@ -12,7 +12,7 @@ tail -3 $OUT/pytest.log
 [ $rc -eq 0 ] || exit $rc
 ROUNDS=4 timeout -k 10 400 bash tools/ab_time.sh "--steps 30 --warmup 3" tree tree:SVH_PIPE_TM=2 tree:SVH_PIPE_TM=3 tree:SVH_PIPE_TM=4 > $OUT/ab.log 2>&1 || { cat $OUT/ab.log; exit 1; }
 cat $OUT/ab.log
-for tm in 3 4; do
+for tm in 2 3 4; do
     for d in 1 3; do
         SVH_PIPE_TM=$tm SVH_LIB=build_ab/d/libspec_viterbi_hip.so SVH_PIPE_DEBUG=$d timeout -k 10 120 python3 tools/launch.py --steps 1 --warmup 1 > $OUT/stamps_tm${tm}_$d.log 2>&1 || { tail $OUT/stamps_tm${tm}_$d.log; exit 1; }
         echo "tm$tm debug=$d: $(grep 'pipe wall' $OUT/stamps_tm${tm}_$d.log | tail -1) | $(grep 'pipe stamps' $OUT/stamps_tm${tm}_$d.log | tail -1)"
