@@ -507,7 +507,7 @@ def main(argv=None):
     # host-to-host, rank 0 only, after the timed region: symbols in the device format (packed uint8,
     # what svh_reader_next yields; svh_viterbi_u8: H2D, run, D2H of scores and best states), and
     # from the reader's list of uint64 arrays (svh_viterbi_seqs, narrowed on the host per call)
-    e2e_ms = e2e_list_ms = None
+    e2e_ms = e2e_list_ms = e2e_pageable_ms = None
     if rank == 0 and seqs and not strong:
         from spec_viterbi_amd.hmm import pack_sequences
         offs, sym64 = pack_sequences(seqs)
@@ -521,14 +521,17 @@ def main(argv=None):
                 f()
                 ts.append(time.perf_counter() - t_e)
             return float(np.median(ts)) * 1e3
-        e2e_ms = med(lambda: model.viterbi_packed(offs, sym8, level=args.level))
+        # results into page-locked arrays (svh_host_alloc): the DMA engine writes them directly
+        out = (svh.pinned_empty((len(seqs), n), np.float32), svh.pinned_empty(len(seqs), np.int64))
+        e2e_ms = med(lambda: model.viterbi_packed(offs, sym8, level=args.level, out=out))
+        e2e_pageable_ms = med(lambda: model.viterbi_packed(offs, sym8, level=args.level))
         e2e_list_ms = med(lambda: model.viterbi(seqs, level=args.level))
 
     if rank == 0:
         nnz = int(info["nnz"])
         lengths = [int(x.size) for x in seqs]
         algo = algorithmic_bytes_per_launch(n, nnz, lengths, args.level, args.paths)
-        kname = (KERNEL_NAMES.get(info["paths_kernel"], "?") + "+traceback" if args.paths
+        kname = (KERNEL_NAMES.get(plan["kernel"], "?") + "+traceback" if args.paths
                  else "spec_chunk+" + KERNEL_NAMES.get(plan["kernel"], "?") if args.level >= 2
                  else KERNEL_NAMES.get(plan["kernel"], "?"))
         pmc = None
@@ -575,6 +578,7 @@ def main(argv=None):
                 "setup_ms": round(float(np.median(setup)) * 1e3, 3),
                 "e2e_ms_per_step": None if e2e_ms is None else round(e2e_ms, 3),
                 "e2e_over_kernel_ms": None if e2e_ms is None else round(e2e_ms - kernel_ms, 3),
+                "e2e_pageable_out_ms_per_step": None if e2e_pageable_ms is None else round(e2e_pageable_ms, 3),
                 "e2e_list_u64_ms_per_step": None if e2e_list_ms is None else round(e2e_list_ms, 3),
                 "e2e_M_state_updates_per_s": None if not e2e_ms else round(updates_per_rank / e2e_ms / 1e3, 2),
                 "setup_plus_e2e_M_state_updates_per_s": None if not e2e_ms else
@@ -582,9 +586,11 @@ def main(argv=None):
                 "gather_ms": round(gather_ms, 3) if gather_ms is not None else None,
                 "note": "setup_ms = svh_model_create (host CSR + plans + upload; the reference rebuilds its model inside "
                         "every run_Viterbi call, bench_Viterbi.h:53-56); e2e = svh_viterbi_u8 from host symbols in the device "
-                        "format (packed uint8, as svh_reader_next yields them) to host scores and best states (batch "
-                        "upload, run, D2H), median of 9 on rank 0; e2e_list_u64 = the same from the reader's list of "
-                        "uint64 arrays (svh_viterbi_seqs, narrowed per call)",
+                        "format (packed uint8, as svh_reader_next yields them) to host scores and best states in "
+                        "page-locked arrays (svh_host_alloc; batch upload, run, D2H straight into them), median of 9 "
+                        "on rank 0; e2e_pageable_out = the same into fresh numpy arrays (staged D2H + copy-out); "
+                        "e2e_list_u64 = from the reader's list of uint64 arrays (svh_viterbi_seqs, narrowed per "
+                        "call), pageable outputs",
             },
             "roofline": rl,
         }

@@ -158,9 +158,15 @@ int svh_batch_run(svh_batch_t b, uint32_t level, void* stream);
  * (nullable) = segments that were re-run.  Synchronous (one host wait at the end). */
 int svh_batch_run_time_parallel(svh_batch_t b, uint32_t seg_len, uint32_t probe_len, float rel_tol,
                                 void* stream, uint64_t* fallbacks);
-/* Synchronise `stream` and copy results to host (any pointer may be NULL). */
+/* Synchronise `stream` and copy results to host (any pointer may be NULL).  Scores and paths
+ * buffers from svh_host_alloc (pinned) are written by the DMA engine directly; pageable buffers
+ * are filled from the batch's pinned staging after the copy. */
 int svh_batch_read(svh_batch_t b, void* stream, float* scores /* nseq * n */,
                    int64_t* best_state /* nseq */, int32_t* paths /* offsets[nseq] */);
+/* Page-locked host memory for result buffers (svh_batch_read / svh_viterbi* write into it without
+ * a staging copy).  svh_host_free releases it. */
+int svh_host_alloc(size_t bytes, void** out);
+int svh_host_free(void* p);
 /* Device pointers of the results (for device-side gathers). */
 int svh_batch_device_results(svh_batch_t b, float** scores, int64_t** best_state);
 /* Milliseconds between the start and stop events of the last svh_batch_run (synchronises). */

@@ -85,6 +85,8 @@ SIGNATURES = {
     "svh_batch_create": (c_int, [c_void_p, c_uint64, P_u64, P_u64, c_uint32, POINTER(c_void_p)]),
     "svh_batch_run": (c_int, [c_void_p, c_uint32, c_void_p]),
     "svh_batch_read": (c_int, [c_void_p, c_void_p, P_f32, P_i64, P_i32]),
+    "svh_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),
+    "svh_host_free": (c_int, [c_void_p]),
     "svh_batch_device_results": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
     "svh_batch_elapsed_ms": (c_int, [c_void_p, P_f32]),
     "svh_batch_plan": (c_int, [c_void_p, c_uint32, POINTER(svh_model_info)]),

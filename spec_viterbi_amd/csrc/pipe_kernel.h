@@ -92,6 +92,17 @@ __device__ __forceinline__ void wait_vmcnt() {
 #define SVH_PIPE_LDSX 1
 #endif
 
+// XCD-local hand-offs (A/B knob SVH_PIPE_XL): every workgroup publishes its XCC id; a granule
+// producer whose consumer workgroup sits on the same XCD stores its granules with plain stores
+// (kept in the XCD's L2) instead of agent-scope write-through stores (which drop the line, so the
+// consumer's L2-served load goes to the fabric), and a consumer on its producer's XCD does the same
+// with its progress word.  The reading side is unchanged (agent-scope loads: L1 bypassed, served
+// by the L2 the plain store wrote); a pair on different XCDs, or one whose id is not known yet,
+// keeps write-through stores.
+#ifndef SVH_PIPE_XL
+#define SVH_PIPE_XL 0
+#endif
+
 // The granule consumer's progress store (once per 32 observations, after the prefetch of the last
 // group) is a vector-memory operation too: the next iteration's first two groups have it queued
 // after their own prefetch, so they wait for one operation more than kGpf - 1, or the in-order
@@ -265,6 +276,11 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     const uint32_t id = (uint32_t)uniform((int)*tick);
     const uint32_t q = id / G, g = id - q * G;
     const uint32_t ep = (uint32_t)uniform((int)__hip_atomic_load(x.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+#if SVH_PIPE_XL
+    const uint32_t my_xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xFu;  // hwreg(HW_REG_XCC_ID, 0, 4)
+    if (tid == 0 && x.xcc)
+        __hip_atomic_store(x.xcc + (size_t)q * G + g, (ep << 4) | my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 
     const uint8_t* __restrict__ sym = b.symbols + b.sym_off[q];
     const uint32_t len = (uint32_t)uniform((int)b.end[q]);
@@ -699,6 +715,31 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         float bprev = kInf;  // boundary score of observation t-1 for the next step (uniform)
 
         auto give_up = [&]() -> bool { return ++spins > kSpinLimit; };
+        // SVH_PIPE_XL: is workgroup og of this row on this wave's XCD?  (bounded poll of its id; not
+        // known in time: no, i.e. write-through stores, always correct)
+        auto xcc_local = [&](uint32_t og) -> bool {
+#if SVH_PIPE_XL
+            if (!x.xcc) return false;
+            const uint32_t* p = x.xcc + (size_t)q * G + og;
+            for (int i = 0; i < 32; ++i) {
+                const uint32_t wv = (uint32_t)uniform((int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if ((wv >> 4) == (ep & 0x0FFFFFFFu)) return (wv & 0xFu) == my_xcc;
+                __builtin_amdgcn_s_sleep(4);
+            }
+#endif
+            (void)og;
+            return false;
+        };
+        bool gran_plain = false, cons_plain = false;
+        // granule / progress-word stores: plain when the reader shares this XCD (SVH_PIPE_XL)
+        auto st_gran = [&](uint64_t* a, uint64_t v64) {
+            if (SVH_PIPE_XL && gran_plain) *a = v64;
+            else g_st64(a, v64);
+        };
+        auto st_cons = [&](uint64_t v64) {
+            if (SVH_PIPE_XL && cons_plain) *cons_in = v64;
+            else g_st64(cons_in, v64);
+        };
         // wait until the previous wave has published observations < need
         auto wait_prev = [&](uint32_t need) {
             while ((uint32_t)uniform((int)lds_ld32(cnt_w - 1)) < need) {
@@ -790,6 +831,8 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 }
             };
 
+            if constexpr (SVH_PIPE_XL && DST == 2) gran_plain = xcc_local(g + 1);
+            if constexpr (SVH_PIPE_XL && SRC == 2) cons_plain = xcc_local(g - 1);
             // publish the state at first-1 and fetch the boundary of first-1
             ring_put(first - 1, v[SM - 1]);
             if constexpr (DST == 2) put_gran1(first - 1, readlane_f(v[SM - 1], 63));
@@ -933,7 +976,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             if constexpr (SVH_PIPE_LDSX && SVH_PIPE_RING8 && k == 3) __builtin_amdgcn_sched_barrier(0);
                             if constexpr (DST == 2 && kGst != 0 && k == kGst) {  // the last group's granules
                                 if (gpend_t && lane < 8)
-                                    g_st64(gout + ((gpend_t + lane) & (kGR - 1)),
+                                    st_gran(gout + ((gpend_t + lane) & (kGR - 1)),
                                            ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
                                 gpend_t = 0;
                             }
@@ -959,14 +1002,14 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             // granules of the previous group (read back from the ring one group ago)
                             if constexpr (kGst == 0) {
                                 if (gpend_t && lane < 8)
-                                    g_st64(gout + ((gpend_t + lane) & (kGR - 1)),
+                                    st_gran(gout + ((gpend_t + lane) & (kGR - 1)),
                                            ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
                             }
                             gpend = ring_w[ring_idx(8 * j + (lane & 7u), 63)];
                             gpend_t = tg;
                         }
                         if constexpr (SRC == 2 && j == 3) {
-                            if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | (tg + 8));
+                            if (lane == 0) st_cons(((uint64_t)ep << 32) | (tg + 8));
                         }
                     };
                     group(std::integral_constant<uint32_t, 0>{}, sw0);
@@ -985,7 +1028,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 if constexpr (SRC == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the prefetches
                 if constexpr (DST == 2) {
                     if (gpend_t && lane < 8)
-                        g_st64(gout + ((gpend_t + lane) & (kGR - 1)),
+                        st_gran(gout + ((gpend_t + lane) & (kGR - 1)),
                                ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
                 }
             }

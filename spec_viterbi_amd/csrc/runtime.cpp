@@ -876,12 +876,14 @@ void PipeScratchBuffers::ensure(uint32_t rows, uint32_t G, hipStream_t s) {
     zeroed(d_gran, (size_t)rows * std::max<uint32_t>(G - 1, 1) * kPipeGRing * 8);
     zeroed(d_cons, (size_t)rows * G * 8);
     zeroed(d_viol, (size_t)rows * 4);
+    zeroed(d_xcc, (size_t)rows * G * 4);
     view.ctr = d_ctr.as<uint32_t>();
     view.done = d_done.as<uint32_t>();
     view.part = d_part.as<uint64_t>();
     view.gran = d_gran.as<uint64_t>();
     view.cons = d_cons.as<uint32_t>();
     view.viol = d_viol.as<uint32_t>();
+    view.xcc = d_xcc.as<uint32_t>();
     view.rows = rows;
     view.G = G;
 }
@@ -891,6 +893,7 @@ void PipeScratchBuffers::note_launch(hipStream_t s) {
         hip_check(hipMemsetAsync(d_ctr.ptr, 0, d_ctr.bytes, s), "pipe epoch reset");
         hip_check(hipMemsetAsync(d_gran.ptr, 0, d_gran.bytes, s), "pipe epoch reset");
         hip_check(hipMemsetAsync(d_cons.ptr, 0, d_cons.bytes, s), "pipe epoch reset");
+        hip_check(hipMemsetAsync(d_xcc.ptr, 0, d_xcc.bytes, s), "pipe epoch reset");
     }
     ++launches;
 }
@@ -1827,6 +1830,16 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
     ran = true;
 }
 
+// Page-locked host memory (hipHostMalloc / hipHostRegister): the DMA engine can write it directly.
+static bool is_pinned_host(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error on some runtimes: clear it
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 void Batch::read(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out) {
     DeviceGuard g(model->device);
     if (!s) s = model->stream;
@@ -1843,18 +1856,25 @@ void Batch::read(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out
     uint8_t* st = h_out.reserve(path_off + pb);
     // One copy, one synchronisation, then out to the caller.  (Four pieces with an event each, the
     // host copying one out while the next moved, were slower: 83 vs 42 us for the headline's 482 KB,
-    // profiles/r04_s8/e2e_split.json.)
-    hip_check(hipMemcpyAsync(st, d_out.ptr, pre, hipMemcpyDeviceToHost, s), "results D2H");
-    if (pb) hip_check(hipMemcpyAsync(st + path_off, d_paths.ptr, pb, hipMemcpyDeviceToHost, s), "paths D2H");
+    // profiles/r04_s8/e2e_split.json.)  Page-locked destinations (svh_host_alloc) take the scores
+    // and paths straight from the DMA engine: no staging, no copy-out.
+    const bool sd = sb && is_pinned_host(scores), pd = pb && is_pinned_host(paths_out);
+    const size_t pre_st = sd ? (bb ? best_off + bb : 16) : pre;  // staged part of the arena
+    hip_check(hipMemcpyAsync(st, d_out.ptr, pre_st, hipMemcpyDeviceToHost, s), "results D2H");
+    if (sd) hip_check(hipMemcpyAsync(scores, p_scores, sb, hipMemcpyDeviceToHost, s), "scores D2H");
+    if (pb)
+        hip_check(hipMemcpyAsync(pd ? reinterpret_cast<uint8_t*>(paths_out) : st + path_off, d_paths.ptr, pb,
+                                 hipMemcpyDeviceToHost, s),
+                  "paths D2H");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     {
         uint32_t f;
         std::memcpy(&f, st, sizeof(f));
         report_fault(f, s);
     }
-    if (sb) std::memcpy(scores, st + score_off, sb);
+    if (sb && !sd) std::memcpy(scores, st + score_off, sb);
     if (bb) std::memcpy(best, st + best_off, bb);
-    if (pb) std::memcpy(paths_out, st + path_off, pb);
+    if (pb && !pd) std::memcpy(paths_out, st + path_off, pb);
 }
 
 void Batch::read_async(hipStream_t s, float* scores, int64_t* best, int32_t* paths_out) {

@@ -182,7 +182,7 @@ struct Pinned {
 
 // Scratch of the pipelined kernel, owned by a batch (grow-only).
 struct PipeScratchBuffers {
-    DeviceBuffer d_ctr, d_done, d_part, d_gran, d_cons, d_viol;
+    DeviceBuffer d_ctr, d_done, d_part, d_gran, d_cons, d_viol, d_xcc;
     PipeScratch view{};
     uint64_t launches = 0;  // pipelined launches on this scratch (its device epoch counts the same)
     void ensure(uint32_t rows, uint32_t G, hipStream_t s);

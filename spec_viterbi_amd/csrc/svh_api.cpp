@@ -242,6 +242,20 @@ int svh_batch_run_time_parallel(svh_batch_t b, uint32_t seg_len, uint32_t probe_
     });
 }
 
+int svh_host_alloc(size_t bytes, void** out) {
+    return guarded([&] {
+        require(out != nullptr, "null argument");
+        *out = nullptr;
+        svh::hip_check(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault), "hipHostMalloc");
+    });
+}
+
+int svh_host_free(void* p) {
+    return guarded([&] {
+        if (p) svh::hip_check(hipHostFree(p), "hipHostFree");
+    });
+}
+
 int svh_batch_read(svh_batch_t b, void* stream, float* scores, int64_t* best_state,
                    int32_t* paths) {
     return guarded([&] {

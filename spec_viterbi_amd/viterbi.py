@@ -26,6 +26,22 @@ def _p(a, t):
     return a.ctypes.data_as(t)
 
 
+def pinned_empty(shape, dtype=np.float32) -> np.ndarray:
+    """An uninitialised array in page-locked host memory (svh_host_alloc): result buffers the DMA
+    engine writes directly (DeviceModel.viterbi_packed(out=...), DeviceBatch.read(out=...)), with
+    no staging copy.  The memory is freed when the array (and every view of it) is gone."""
+    import weakref
+
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape)) * dtype.itemsize
+    ptr = ctypes.c_void_p()
+    _lib.check(_lib.lib.svh_host_alloc(max(n, 1), ctypes.byref(ptr)))
+    buf = (ctypes.c_uint8 * max(n, 1)).from_address(ptr.value)
+    arr = np.frombuffer(buf, np.uint8, count=n).view(dtype).reshape(shape)
+    weakref.finalize(buf, _lib.lib.svh_host_free, ptr.value)
+    return arr
+
+
 class DeviceModel:
     """An HMM resident in HBM on one device (svh_model_create)."""
 
@@ -80,13 +96,21 @@ class DeviceModel:
             return scores, best, [pth[offsets[q]:offsets[q + 1]] for q in range(nseq)]
         return scores, best
 
-    def viterbi_packed(self, offsets, symbols, level: int = 0, paths: bool = False):
+    def viterbi_packed(self, offsets, symbols, level: int = 0, paths: bool = False, out=None):
         """One-shot over packed sequences: offsets [nseq+1] and uint8 symbols (the device format,
-        svh_viterbi_u8; e.g. what svh_reader_next returns) or uint64 symbols (svh_viterbi)."""
+        svh_viterbi_u8; e.g. what svh_reader_next returns) or uint64 symbols (svh_viterbi).
+        `out` = (scores [nseq, n] float32, best [nseq] int64) to fill instead of new arrays;
+        arrays from pinned_empty take the scores straight from the DMA engine."""
         offsets = np.ascontiguousarray(offsets, np.uint64)
         nseq = offsets.size - 1
-        scores = np.empty((nseq, self.n), np.float32)
-        best = np.empty(nseq, np.int64)
+        if out is not None:
+            scores, best = out
+            if (scores.shape != (nseq, self.n) or scores.dtype != np.float32 or not scores.flags.c_contiguous
+                    or best.shape != (nseq,) or best.dtype != np.int64 or not best.flags.c_contiguous):
+                raise ValueError("out: (float32 [nseq, n], int64 [nseq]) C-contiguous arrays expected")
+        else:
+            scores = np.empty((nseq, self.n), np.float32)
+            best = np.empty(nseq, np.int64)
         pth = np.empty(int(offsets[-1] - offsets[0]) if nseq else 0, np.int32) if paths else None
         symbols = np.asarray(symbols)
         if symbols.dtype == np.uint8:

@@ -3,6 +3,7 @@
 Scores must be bit-identical to GraphBLAS_impl's association (-0.0 == +0.0), best states and
 decoded paths identical (lowest index on ties).
 """
+import ctypes
 import os
 
 import numpy as np
@@ -501,3 +502,46 @@ def test_oneshot_symbol_forms_agree():
     # and the model still answers afterwards
     scores, best = model.viterbi(seqs)
     assert all(bit_equal(scores[q], got["seqs"][0][q]) for q in range(len(seqs)))
+
+
+def test_results_into_pinned_buffers():
+    """svh_batch_read / svh_viterbi_u8 into page-locked arrays (svh_host_alloc: the DMA engine
+    writes the scores directly, no staging): the headline batch's rows equal the digests and the
+    pageable path's results, repeated calls overwrite the same buffers, paths too."""
+    import hashlib
+
+    from spec_viterbi_amd.hmm import pack_sequences
+    from tests.helpers import load_digests
+
+    rows = load_digests()["2405.chmm x emit_50_3500_20.ess"]
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
+    model = svh.DeviceModel(hmm)
+    offs, sym64 = pack_sequences(seqs)
+    sym8 = sym64.astype(np.uint8)
+    out = (svh.pinned_empty((len(seqs), model.n), np.float32), svh.pinned_empty(len(seqs), np.int64))
+    for _ in range(2):
+        out[0].fill(np.nan)
+        out[1].fill(-7)
+        s, b = model.viterbi_packed(offs, sym8, out=out)
+        assert s is out[0] and b is out[1]
+        for q in range(len(seqs)):
+            assert hashlib.sha256(np.ascontiguousarray(s[q]).tobytes()).hexdigest() == rows[q]["scores_sha256"], q
+            assert b[q] == rows[q]["best_state"], q
+    sp, bp = model.viterbi_packed(offs, sym8)
+    assert np.array_equal(sp.view(np.uint32), out[0].view(np.uint32)) and np.array_equal(bp, out[1])
+    # a batch read with a pinned score buffer and a pinned path buffer
+    short = [x[:300] for x in seqs[:4]]
+    batch = model.batch(short, paths=True)
+    batch.run()
+    ref_s, ref_b, ref_p = batch.read(want_paths=True)
+    ps = svh.pinned_empty((len(short), model.n), np.float32)
+    pb = np.empty(len(short), np.int64)
+    pp = svh.pinned_empty(sum(x.size for x in short), np.int32)
+    _lib.check(_lib.lib.svh_batch_read(batch._h, None, ps.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                       pb.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                       pp.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+    assert np.array_equal(ps.view(np.uint32), ref_s.view(np.uint32)) and np.array_equal(pb, ref_b)
+    assert np.array_equal(pp, np.concatenate(ref_p))
+    with pytest.raises(ValueError):
+        model.viterbi_packed(offs, sym8, out=(out[0][:3], out[1]))

@@ -58,6 +58,8 @@ def main():
     res = {}
     res["list_seqs_ms"] = med(lambda: model.viterbi(seqs), a.reps)
     res["packed_u8_ms"] = med(lambda: model.viterbi_packed(offs, sym8), a.reps)
+    pout = (svh.pinned_empty((len(seqs), model.n), np.float32), svh.pinned_empty(len(seqs), np.int64))
+    res["packed_u8_pinned_out_ms"] = med(lambda: model.viterbi_packed(offs, sym8, out=pout), a.reps)
     res["packed_u64_ms"] = med(lambda: model.viterbi_packed(offs, sym64), a.reps)
 
     def old_path():  # round 3: pack in Python, then svh_viterbi
@@ -70,6 +72,7 @@ def main():
     res["pack_plus_u64_ms"] = med(old_path, a.reps)
     res["python_pack_ms"] = med(lambda: pack_sequences(seqs), a.reps)
     checks = {"list": ok(model.viterbi(seqs)[0]), "u8": ok(model.viterbi_packed(offs, sym8)[0]),
+              "u8_pinned": ok(model.viterbi_packed(offs, sym8, out=pout)[0]),
               "u64": ok(model.viterbi_packed(offs, sym64)[0]), "old": ok(old_path())}
 
     batch = model.batch(seqs)
@@ -92,6 +95,7 @@ def main():
     res["checks"] = checks
     res["overhead_list_ms"] = res["list_seqs_ms"] - res["kernel_ms"]
     res["overhead_u8_ms"] = res["packed_u8_ms"] - res["kernel_ms"]
+    res["overhead_u8_pinned_out_ms"] = res["packed_u8_pinned_out_ms"] - res["kernel_ms"]
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in res.items()}), flush=True)
     batch.close()
     model.close()
