@@ -231,6 +231,7 @@ struct PipeScratch {
     uint32_t* cons;   // [rows][G] granules received by workgroup g's first wave
     uint32_t* viol;   // [rows] 1: speculation failed, row needs the serial kernel
     uint32_t* xcc;    // [rows][G] (epoch << 4) | XCC id of workgroup g of row q (XCD-local hand-offs)
+    uint32_t xmap;    // launch: 1 = (row, workgroup) from blockIdx by XCD class (every workgroup resident)
     uint32_t rows, G;
 };
 constexpr uint32_t kPairSymbols = 20;  // pipe_kernel.h kPairSym: the pair tables' symbol capacity

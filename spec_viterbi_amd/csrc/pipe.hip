@@ -3,6 +3,8 @@
 // the pair-table variant (TM = 1).
 #include "pipe_kernel.h"
 
+#include <cstdlib>
+
 namespace svh {
 
 namespace {
@@ -56,6 +58,10 @@ hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratc
     PipeScratch xx = x;
     void* args[] = {&mm, &bb, &xx};
     const uint64_t grid = (uint64_t)b.nseq * m.G;
+    // XCD-class mapping of rows to workgroups while the launch is resident at one workgroup per
+    // CU (pipe_kernel.h); SVH_PIPE_XMAP=0 keeps the dynamic tickets (A/B)
+    static const bool xmap_env = !(std::getenv("SVH_PIPE_XMAP") && std::atoi(std::getenv("SVH_PIPE_XMAP")) == 0);
+    xx.xmap = xmap_env && m.cus && grid <= m.cus ? 1u : 0u;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const size_t lds = paths ? (pipe_lds_bytes(m.W, m.S) + 15) / 16 * 16 + pipe_path_lds_bytes(m.W)
                              : pipe_lds_bytes(m.W, m.S);

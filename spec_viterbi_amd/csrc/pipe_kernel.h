@@ -82,7 +82,8 @@ __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// LDS reads of the exchange kept where they are issued (A/B knob SVH_PIPE_LDSX, default 1): the
+// LDS reads of the exchange kept where they are issued (A/B knob SVH_PIPE_LDSX, default 1; within
+// run-to-run noise on the headline, 0.258-0.265 vs 0.256-0.264 ms, profiles/r04_s9/ab.log): the
 // compiler otherwise (a) hoisted the slow path's re-load of the next group's boundary vector out of
 // its branch, so every group re-read it at its first use and waited for it there, and (b) moved the
 // readfirstlane of the neighbours' counts (read four steps before their use) up to the reads,
@@ -98,9 +99,10 @@ __device__ __forceinline__ void wait_vmcnt() {
 // consumer's L2-served load goes to the fabric), and a consumer on its producer's XCD does the same
 // with its progress word.  The reading side is unchanged (agent-scope loads: L1 bypassed, served
 // by the L2 the plain store wrote); a pair on different XCDs, or one whose id is not known yet,
-// keeps write-through stores.
+// keeps write-through stores.  Measured on the headline: 0.248-0.251 ms against 0.258-0.265
+// (profiles/r04_s9/ab.log); the XCD half whose hops were slow (§5f) comes down to the other's rate.
 #ifndef SVH_PIPE_XL
-#define SVH_PIPE_XL 0
+#define SVH_PIPE_XL 1
 #endif
 
 // The granule consumer's progress store (once per 32 observations, after the prefetch of the last
@@ -273,7 +275,33 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     if (tid < 16) cnt[tid] = 0;
     for (uint32_t i = tid; i < S * 8; i += 64 * W) ctab[i] = m.hc[i];
     __syncthreads();
-    const uint32_t id = (uint32_t)uniform((int)*tick);
+    // (row, workgroup) of this workgroup.  Dynamic tickets in start order by default (a consumer's
+    // producer has always started: no deadlock when the grid exceeds residency).  x.xmap (the
+    // runtime sets it only when every workgroup of the launch is resident): by blockIdx, so that
+    // a row's G workgroups share an XCD class (blocks b and b + 8 share an XCD under the observed
+    // round-robin placement; speed only -- the hand-offs check the real XCC ids, SVH_PIPE_XL):
+    // class r = b % 8 takes rows whole, G consecutive members each, and the classes' leftover
+    // members form the remaining rows in class order.
+    uint32_t id = (uint32_t)uniform((int)*tick);
+    if (x.xmap) {
+        const uint32_t N = gridDim.x, r = blockIdx.x & 7u, k = blockIdx.x >> 3;
+        uint32_t pf = 0, po = 0, fr = 0, F = 0;
+        for (uint32_t rr = 0; rr < 8; ++rr) {
+            const uint32_t n = N > rr ? (N - rr + 7) / 8 : 0, f = n / G;
+            F += f;
+            if (rr < r) {
+                pf += f;
+                po += n - f * G;
+            }
+            if (rr == r) fr = f;
+        }
+        if (k < fr * G) {
+            id = (pf + k / G) * G + k % G;
+        } else {
+            const uint32_t u = po + (k - fr * G);
+            id = (F + u / G) * G + u % G;
+        }
+    }
     const uint32_t q = id / G, g = id - q * G;
     const uint32_t ep = (uint32_t)uniform((int)__hip_atomic_load(x.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
 #if SVH_PIPE_XL

@@ -997,6 +997,7 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
         int cus = 0;
         hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device), "CU count");
         cu_count = (uint32_t)cus;
+        if (pipe.plan.ok) pipe.view.cus = cu_count;  // latency plan: the XCD-class mapping's residency test
         if (pipe.plan.ok) {
             // AUTO: the latency plan while the batch gives every CU at most one of its workgroups
             // (one wave per SIMD); wider batches run the wide pipelined plan (measured: DESIGN.md
