@@ -523,9 +523,9 @@ def main(argv=None):
             return float(np.median(ts)) * 1e3
         # results into page-locked arrays (svh_host_alloc): the DMA engine writes them directly
         out = (svh.pinned_empty((len(seqs), n), np.float32), svh.pinned_empty(len(seqs), np.int64))
-        e2e_ms = med(lambda: model.viterbi_packed(offs, sym8, level=args.level, out=out))
-        e2e_pageable_ms = med(lambda: model.viterbi_packed(offs, sym8, level=args.level))
-        e2e_list_ms = med(lambda: model.viterbi(seqs, level=args.level))
+        e2e_ms = med(lambda: model.viterbi_packed(offs, sym8, level=args.level, paths=args.paths, out=out))
+        e2e_pageable_ms = med(lambda: model.viterbi_packed(offs, sym8, level=args.level, paths=args.paths))
+        e2e_list_ms = med(lambda: model.viterbi(seqs, level=args.level, paths=args.paths))
 
     if rank == 0:
         nnz = int(info["nnz"])
