@@ -64,7 +64,11 @@ hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratc
     xx.xmap = xmap_env && m.cus && grid <= m.cus ? 1u : 0u;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const size_t lds = paths ? (pipe_lds_bytes(m.W, m.S) + 15) / 16 * 16 + pipe_path_lds_bytes(m.W)
-                             : pipe_lds_bytes(m.W, m.S);
+                             : pipe_lds_bytes(m.W, m.S)
+#ifdef SVH_PIPE_G16  // A/B experiment: the 64-slot ring of pipe_kernel_g16.h
+                                   + (size_t)m.W * 32 * 64 * 4
+#endif
+        ;
     if (lds > 64 * 1024) {  // more than 64 KiB of dynamic LDS: a host-side attribute of the function
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

@@ -1,0 +1,1210 @@
+// EXPERIMENT (A/B build only: pipe_tm1.hip with -DSVH_PIPE_G16): pipe_kernel.h with exchange
+// groups of 16 observations instead of 8 (half the per-observation exchange work), a 64-slot LDS
+// ring and one granule group prefetched ahead.  Scores only (PATHS = 0).  Not in the default build.
+//
+// Pipelined chain Viterbi kernel (gfx950): the latency path for MSV-shaped models whose feeder row
+// F (N) is speculated and verified exactly (kernels.h, PipeModel).
+//
+// Reference hot loop: Viterbi_impl/GraphBLAS_impl.cpp:59-73 (same association, bit-identical):
+//     v'[j] = min_k fl( fl(E[o][j] + T^T[j][k]) + v[k] )
+// For the light rows of the chain shape this is v'_p = min(fl(eb_p(o) + v_{p-1}), fl(ea_p(o) + F))
+// with eb_p(o) = fl(E_o[p] + bw_p), ea_p(o) = fl(E_o[p] + aw_p) (the reference's first add, folded
+// into the table), so once F's sequence is known a position depends only on its chain predecessor
+// one observation earlier: a wavefront over (position block, observation) with no feedback.
+//
+// Geometry: block b = 64*SM consecutive positions, one wave (lane l holds positions
+// b*64*SM + l*SM + s); W blocks per workgroup, G = ceil(nblk / W) workgroups per sequence.
+// Each wave sweeps all observations of its block.  Its last position's score of observation t
+// is the chain input of the next block's position 0 at t+1:
+//   * within a workgroup: every lane writes its score into an LDS ring [kPipeRing][64] each
+//     observation; the wave publishes "observations done" once per group of 8; the consumer
+//     waits for the whole group, reads its 8 boundary values with one ds_read and extracts them
+//     with v_readlane (one per observation); producers check the consumer's count once per
+//     group before reusing ring slots.
+//   * between workgroups: the last wave stores 8-byte granules {score, tag} (agent scope, sc1)
+//     into a ring of kPipeGRing per sequence boundary; the next workgroup's first wave keeps
+//     kPipeAhead groups of granule loads in flight and checks the tags; flow control through a
+//     tagged progress word.  Workgroups take dynamic tickets in start order, so a consumer's
+//     producer always started first (no deadlock when the grid exceeds residency).
+// Per lane and observation the heavy side is: S partial  c' = min(fl(A_S + m), fl(X_SS + c)
+// [, fl(X_SF + F)]) with m = min of the lane's scores at t-1 (exact: S(t) = min over lanes of c,
+// fl(a + .) is monotone), F' = fl(X_FF + F), and the check fl(A_F + m) < F' (a violation: F
+// would have taken its light term, the speculation and everything after it is void).
+// The last workgroup of a sequence to finish combines the partials (S, argmin, violation).
+//
+// Decoded paths (PATHS = 1, 2): per observation and light position the "took F's term" bit
+// (compare into VCC + v_addc into a per-lane word per slot, stored every 32 observations; PATHS 2
+// when F wins every tie: one compare), per observation the lane's {light minimum of t-1, sink
+// partial of t} into an LDS ring that the wave folds every 32 observations into per-half-wave
+// partial records (transposed: lane l reduces row l % 32 over its half), light-score checkpoints
+// every kCkptEvery observations and F every 32 (block 0).  pipe_paths.hip turns these into the
+// heavy records and walks the paths.
+#pragma once
+#include "pipe_common.h"
+
+namespace svh {
+
+using namespace dev;
+using namespace pipe_dev;
+
+namespace {
+
+typedef float f32x32 __attribute__((ext_vector_type(32)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+constexpr uint32_t kR = 64;  // G16: four groups of 16 in the ring
+constexpr uint32_t kG = 16;
+#ifndef SVH_PIPE_G16_CNT
+#define SVH_PIPE_G16_CNT 8
+#endif
+constexpr uint32_t kGcnt = SVH_PIPE_G16_CNT;  // step of the group at which the neighbours' counts are read
+
+// Granule hand-off between workgroups: groups of 8 granules the consumer keeps in flight ahead of
+// use (1, 2 or 4), and the step of the next group at which the producer stores a finished group's
+// granules (0: at the end of the next group).  A/B knobs (tools/ab_build.sh -D...).
+#ifndef SVH_PIPE_GPF
+#define SVH_PIPE_GPF 2
+#endif
+#ifndef SVH_PIPE_GST
+#define SVH_PIPE_GST 2
+#endif
+constexpr uint32_t kGpf = 1;  // G16: one group (16 observations) ahead
+constexpr uint32_t kGst = SVH_PIPE_GST;
+static_assert(kGpf == 1 || kGpf == 2 || kGpf == 4, "granule prefetch depth");
+static_assert(kGst < 8, "granule store step");
+
+// LDS boundary ring layout: 0 = [u][lane] (every step stores its row, one ds_write_b32; TM = 0,
+// pipe.hip); 1 = [u / 8][lane][u % 8]: a group's 8 last-slot scores stay in registers and go out as
+// two ds_write_b128 per group (the consumer reads lane 63's 8 values as one contiguous 32 bytes;
+// TM = 1 / 2, pipe_tm1.hip and pipe_tm1p.hip define it).
+#ifndef SVH_PIPE_RING8
+#define SVH_PIPE_RING8 0
+#endif
+// ring slot of cycle position u (0..31) and lane l
+__device__ __forceinline__ uint32_t ring_idx(uint32_t u, uint32_t l) {
+    return SVH_PIPE_RING8 ? ((u >> 3) * 64 + l) * 8 + (u & 7u) : u * 64 + l;
+}
+
+template <uint32_t N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N < 64, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS reads of the exchange kept where they are issued (A/B knob SVH_PIPE_LDSX, default 1; within
+// run-to-run noise on the headline, 0.258-0.265 vs 0.256-0.264 ms, profiles/r04_s9/ab.log): the
+// compiler otherwise (a) hoisted the slow path's re-load of the next group's boundary vector out of
+// its branch, so every group re-read it at its first use and waited for it there, and (b) moved the
+// readfirstlane of the neighbours' counts (read four steps before their use) up to the reads,
+// waiting for them at once.  An opaque zero in the slow path's address and an asm use of each count
+// where it is needed keep both reads' latency behind steps.
+#ifndef SVH_PIPE_LDSX
+#define SVH_PIPE_LDSX 1
+#endif
+
+// XCD-local hand-offs (A/B knob SVH_PIPE_XL): every workgroup publishes its XCC id; a granule
+// producer whose consumer workgroup sits on the same XCD stores its granules with plain stores
+// (kept in the XCD's L2) instead of agent-scope write-through stores (which drop the line, so the
+// consumer's L2-served load goes to the fabric), and a consumer on its producer's XCD does the same
+// with its progress word.  The reading side is unchanged (agent-scope loads: L1 bypassed, served
+// by the L2 the plain store wrote); a pair on different XCDs, or one whose id is not known yet,
+// keeps write-through stores.  Measured on the headline: 0.248-0.251 ms against 0.258-0.265
+// (profiles/r04_s9/ab.log); the XCD half whose hops were slow (§5f) comes down to the other's rate.
+#ifndef SVH_PIPE_XL
+#define SVH_PIPE_XL 1
+#endif
+
+// The granule consumer's progress store (once per 32 observations, after the prefetch of the last
+// group) is a vector-memory operation too: the next iteration's first two groups have it queued
+// after their own prefetch, so they wait for one operation more than kGpf - 1, or the in-order
+// vmcnt would make them wait for the younger prefetch (issued one group earlier) as well.  A/B knob
+// (SVH_PIPE_VMS=0: the old count).
+#ifndef SVH_PIPE_VMS
+#define SVH_PIPE_VMS 0
+#endif
+
+// Publishing a wave's count (A/B knob SVH_PIPE_PUT): 0 = one lane's store with EXEC narrowed to
+// lane 0 inside the asm (lds_put1); 1 = every lane stores, lane 0 to the count and lanes 1..63 to
+// a sink of their own (a per-lane address vector built once: no EXEC writes, no s_nop).
+#ifndef SVH_PIPE_PUT
+#define SVH_PIPE_PUT 0
+#endif
+__device__ __forceinline__ void lds_put_v(uint32_t vaddr, uint32_t v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(vaddr), "v"(v) : "memory");
+}
+// One lane's LDS store of a wave-uniform word: EXEC narrowed to lane 0 inside the asm (no
+// divergent branch in the compiler's view).
+__device__ __forceinline__ void lds_put1(uint32_t addr, uint32_t v) {
+    uint64_t saved;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "s_nop 1\n\t"
+        "ds_write_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "v"(addr), "v"(v)
+        : "memory");
+}
+
+// The chain term of slot 0 alone (TM = 2, whose feeder terms come out of the indexed block):
+// xb = fl(eb + (lane ? x[lane-1] : b)), b the SGPR boundary (R < 0), lane 0 of bvv (R = 0) or lane R
+// of bvv (row_ror:16-R).  x was written before the step's indexed block and bvv at the start of
+// the group, so both DPP reads have their wait states (tools/dpp_hazards.py checks every build).
+template <int R>
+__device__ __forceinline__ float chain_b(float eb, float b, float x) {
+    float xb;
+    if constexpr (R < 0) {
+        asm("v_add_f32_e32 %0, %1, %2\n\t"
+            "v_add_f32_dpp %0, %3, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb)
+            : "s"(b), "v"(eb), "v"(x));
+    } else if constexpr (R == 0) {
+        asm("v_add_f32_e32 %0, %1, %2\n\t"
+            "v_add_f32_dpp %0, %3, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb)
+            : "v"(b), "v"(eb), "v"(x));
+    } else {
+        asm("v_add_f32_dpp %0, %1, %2 row_ror:%4 row_mask:0xf bank_mask:0xf\n\t"
+            "v_add_f32_dpp %0, %3, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb)
+            : "v"(b), "v"(eb), "v"(x), "n"(16 - R));
+    }
+    return xb;
+}
+
+// Chain and feeder terms of slot 0: xb = fl(eb + (lane ? x[lane-1] : bnd)), xa = fl(ea + f).
+// The DPP read of x follows two VALU instructions of this block (its two wait states).
+__device__ __forceinline__ void chain_terms(float& xb, float& xa, float eb, float ea, float bnd, float f,
+                                            float x) {
+    asm("v_add_f32_e32 %0, %2, %3\n\t"
+        "v_add_f32_e32 %1, %4, %5\n\t"
+        "v_add_f32_dpp %0, %6, %3 wave_shr:1 row_mask:0xf bank_mask:0xf"
+        : "=&v"(xb), "=&v"(xa)
+        : "s"(bnd), "v"(eb), "v"(f), "v"(ea), "v"(x));
+}
+
+// The same with lane 0's chain input taken from lane R of the group vector bvv (row_ror:16-R
+// rotates lane R of each row of 16 into its lane 0; no SGPR round trip).  xa comes first, so x
+// has its two wait states inside the block; bvv has one inside the block and gets the other from
+// the schedule around it (bvv is written at the start of a group, never by the instruction before
+// a step).  The compiler does not see DPP inside asm, so the build checks every DPP read of the
+// kernel for the two wait states (tools/dpp_hazards.py, Makefile); the s_nop the block carried
+// before cost 1.6 % (A/B 0.361 vs 0.367 ms).
+template <int R>
+__device__ __forceinline__ void chain_terms_v(float& xb, float& xa, float eb, float ea, float bvv, float f,
+                                              float x) {
+    if constexpr (R == 0) {
+        asm("v_add_f32_e32 %1, %4, %5\n\t"
+            "v_add_f32_e32 %0, %2, %3\n\t"
+            "v_add_f32_dpp %0, %6, %3 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb), "=&v"(xa)
+            : "v"(bvv), "v"(eb), "v"(f), "v"(ea), "v"(x));
+    } else {
+        asm("v_add_f32_e32 %1, %4, %5\n\t"
+            "v_add_f32_dpp %0, %2, %3 row_ror:%7 row_mask:0xf bank_mask:0xf\n\t"
+            "v_add_f32_dpp %0, %6, %3 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb), "=&v"(xa)
+            : "v"(bvv), "v"(eb), "v"(f), "v"(ea), "v"(x), "n"(16 - R));  // lane 0 <- lane R
+    }
+}
+
+// TM 3: both feeder terms in one packed add, xa = {ea_0 + F, ea_1 + F} (F = the high half of cf),
+// then slot 0's chain term as chain_terms / chain_terms_v (the packed add and, R < 1, the plain add
+// give the DPP read of x its two wait states inside the block).
+template <int R>
+__device__ __forceinline__ void chain_terms_pk(float& xb, f2& xa, f2 ea, float eb, float bnd, f2 cf, float x) {
+    if constexpr (R < 0) {
+        asm("v_pk_add_f32 %1, %3, %5 op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+            "v_add_f32_e32 %0, %2, %4\n\t"
+            "v_add_f32_dpp %0, %6, %4 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb), "=&v"(xa)
+            : "s"(bnd), "v"(ea), "v"(eb), "v"(cf), "v"(x));
+    } else if constexpr (R == 0) {
+        asm("v_pk_add_f32 %1, %3, %5 op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+            "v_add_f32_e32 %0, %2, %4\n\t"
+            "v_add_f32_dpp %0, %6, %4 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb), "=&v"(xa)
+            : "v"(bnd), "v"(ea), "v"(eb), "v"(cf), "v"(x));
+    } else {
+        asm("v_pk_add_f32 %1, %3, %5 op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+            "v_add_f32_dpp %0, %2, %4 row_ror:%7 row_mask:0xf bank_mask:0xf\n\t"
+            "v_add_f32_dpp %0, %6, %4 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "=&v"(xb), "=&v"(xa)
+            : "v"(bnd), "v"(ea), "v"(eb), "v"(cf), "v"(x), "n"(16 - R));  // lane 0 <- lane R
+    }
+}
+
+// Table reads of a step (template TM):
+//   0  per-slot tables f32x32 [SM][eb|ea] (symbol o in register o): the compiler's indexed moves,
+//      one s_set_gpr_idx block of SM x 2 v_mov, and the heavy constants by four v_readlane;
+//   1  (SM = 2, at most kPairSym symbols) four pair-interleaved tables pinned to v2..v161,
+//      register 2o + u = value u of symbol o: T1 = {eb_0, ea_0}, T2 = {eb_1, ea_1},
+//      T3 = {A_S, A_F}, T4 = {X_SS, X_FF}; one idx block of four v_mov_b64 (M0 = 2o, the symbol
+//      windows are loaded pre-doubled), so no v_readlane and no SGPR hand-off per step;
+//   2  the same tables read as M0-indexed operands of the adds that use them (one gpr_idx(SRC0)
+//      block, only eb_0 moved out for slot 0's DPP chain add);
+//   3  as 1 with T1 = {ea_0, ea_1}, T2 = {eb_0, eb_1}: both feeder terms come out of one
+//      v_pk_add_f32 with F broadcast from the high half of the {C, F} pair (op_sel), one VALU less;
+//   4  as 2 with the layout of 3 (the packed feeder add reads T1 as an indexed 64-bit operand).
+// tools/ubench/step_ubench.hip prices the two at 158 vs 101 shader cycles per observation (no
+// exchange, 4 waves per CU).  Measured and not kept (round 3): every table and constant read as an
+// M0-indexed operand of the add that uses it (13 VALU, 66 vs 72 ns a step, 1 % in the pipeline);
+// indexed adds through gpr_idx(SRC0) with the DPP pair after the block (0.39 ms), everything but the
+// constants through gpr_idx(SRC1) (0.37), the constants by a broadcast ds_read_b128 a step ahead
+// instead of v_readlane (0.38).
+constexpr uint32_t kPairSym = kPairSymbols;
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+// Slot 0's chain input for a step: R < 0 the uniform boundary b (SGPR, single observations),
+// R = 0 lane 0 of the group vector, R = 1..7 lane R of the group vector (row_ror:16-R).
+template <int R>
+struct ChainIn {
+    static constexpr int value = R;
+    float b;
+};
+
+template <int SM, int W, bool SX, int PATHS, int TM>
+__global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
+    static_assert(TM == 0 || SM == 2, "pair tables: two slots per lane");
+    static_assert(TM >= 0 && TM <= 4, "table mode");
+    static_assert(PATHS == 0, "G16 experiment: scores only");
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* ring = lds;                                                  // [W][kR][64]
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(ring + W * kR * 64);    // [16]
+    float* ctab = reinterpret_cast<float*>(cnt + 16);                   // [S][8]
+    float* red = ctab + m.S * 8;                                        // [W][4]
+    uint32_t* tick = reinterpret_cast<uint32_t*>(red + W * 4);
+    // PATHS: [W][32][kPRingStride] rows {pm, c} per lane, 16-byte aligned after the rest
+    float* pring = lds + (pipe_lds_bytes(W, m.S) + 15) / 16 * 4;
+
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t w = (uint32_t)uniform((int)(tid >> 6));
+    const uint32_t S = m.S, P = m.P, G = m.G;
+    if (tid == 0) *tick = __hip_atomic_fetch_add(x.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 16) cnt[tid] = 0;
+    for (uint32_t i = tid; i < S * 8; i += 64 * W) ctab[i] = m.hc[i];
+    __syncthreads();
+    // (row, workgroup) of this workgroup.  Dynamic tickets in start order by default (a consumer's
+    // producer has always started: no deadlock when the grid exceeds residency).  x.xmap (the
+    // runtime sets it only when every workgroup of the launch is resident): by blockIdx, so that
+    // a row's G workgroups share an XCD class (blocks b and b + 8 share an XCD under the observed
+    // round-robin placement; speed only -- the hand-offs check the real XCC ids, SVH_PIPE_XL):
+    // class r = b % 8 takes rows whole, G consecutive members each, and the classes' leftover
+    // members form the remaining rows in class order.
+    uint32_t id = (uint32_t)uniform((int)*tick);
+    if (x.xmap) {
+        const uint32_t N = gridDim.x, r = blockIdx.x & 7u, k = blockIdx.x >> 3;
+        uint32_t pf = 0, po = 0, fr = 0, F = 0;
+        for (uint32_t rr = 0; rr < 8; ++rr) {
+            const uint32_t n = N > rr ? (N - rr + 7) / 8 : 0, f = n / G;
+            F += f;
+            if (rr < r) {
+                pf += f;
+                po += n - f * G;
+            }
+            if (rr == r) fr = f;
+        }
+        if (k < fr * G) {
+            id = (pf + k / G) * G + k % G;
+        } else {
+            const uint32_t u = po + (k - fr * G);
+            id = (F + u / G) * G + u % G;
+        }
+    }
+    const uint32_t q = id / G, g = id - q * G;
+    const uint32_t ep = (uint32_t)uniform((int)__hip_atomic_load(x.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+#if SVH_PIPE_XL
+    const uint32_t my_xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xFu;  // hwreg(HW_REG_XCC_ID, 0, 4)
+    if (tid == 0 && x.xcc)
+        __hip_atomic_store(x.xcc + (size_t)q * G + g, (ep << 4) | my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+
+    const uint8_t* __restrict__ sym = b.symbols + b.sym_off[q];
+    const uint32_t len = (uint32_t)uniform((int)b.end[q]);
+    const uint32_t beg = (uint32_t)uniform((int)b.begin[q]);
+    const uint32_t first = beg ? beg : 1u;  // first observation the steps run (state at first-1)
+    const uint32_t blk = g * W + w;
+    const bool act = blk < m.nblk;
+    const bool lastb = blk + 1 >= m.nblk;
+    // boundary roles: source 0 none (block 0), 1 LDS (previous wave), 2 granules (previous
+    // workgroup); sink 0 none (last block), 1 LDS, 2 granules
+    const int src = blk == 0 ? 0 : (w > 0 ? 1 : 2);
+    const int dst = lastb ? 0 : (w + 1 < (uint32_t)W ? 1 : 2);
+
+    float v[SM];  // light scores of the lane's positions
+    f2 CF;        // {S partial of this lane, F'} (one register pair: the packed heavy update)
+    uint32_t viol = 0;  // per lane: steps whose check failed (a VGPR count: no VALU -> SALU hand-off)
+    uint32_t spins = 0;
+    // PATHS: the last 32 "took F's term" bits per slot (bit 0 = newest), the static tie masks
+    // (PATHS 1), the lane's light minimum of the last step's input scores
+    uint32_t macc[PATHS ? SM : 1] = {};
+    uint64_t pmC[PATHS ? SM : 1] = {};
+    float last_pm = kInf;
+    // diagnostics: 0 loop cycles, 1 head cycles, 2 tail cycles, 3 slow re-reads waiting for the
+    // previous wave, 4 ... for the next wave (flow control), 5 ... for granules, 6 ... for the
+    // consumer's progress word, 7 body iterations, 8 .. 11 the 100 MHz real-time clock at wave
+    // entry, sweep start, body end, sweep end, 12 the wave's XCC_ID << 32 | HW_ID (placement).
+    // Built only with -DSVH_PIPE_DIAG (tools/ab_build.sh;
+    // then SVH_PIPE_DEBUG=1 at run time): the counters would otherwise hold SGPRs through the loop
+    // in the production kernel, whose SGPRs are its scarcest register file.
+    unsigned long long dg[kPipeStamps] = {};
+#ifdef SVH_PIPE_DIAG
+    const bool dbg = m.stamps != nullptr;
+#define SVH_RT(k) (dg[k] = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull)
+#else
+    constexpr bool dbg = false;
+#define SVH_RT(k) ((void)0)
+#endif
+    SVH_RT(8);
+#ifdef SVH_PIPE_DIAG
+    if (dbg)  // hwreg(HW_REG_XCC_ID) and hwreg(HW_REG_HW_ID), 32 bits each
+        dg[12] = ((unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                 (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
+
+    if (act) {
+        const uint32_t p0 = blk * 64 * SM + lane * SM;
+        // ---- tables: (eb, ea) of the lane's positions for every symbol, in VGPRs
+        f32x32 EB[SM], EA[SM];
+#pragma unroll
+        for (int s = 0; s < SM; ++s)
+#pragma unroll
+            for (int o = 0; o < 32; ++o) {
+                // unconditional loads (a clamped symbol), then a select: all 32 x SM loads go out
+                // back to back (a conditional load per symbol serialised them: ~15 us of prologue)
+                const uint32_t oc = (uint32_t)o < S ? (uint32_t)o : S - 1u;
+                const float2 e = m.tab[((size_t)(blk * S + oc) * SM + s) * 64 + lane];
+                EB[s][o] = (uint32_t)o < S ? e.x : kInf;
+                EA[s][o] = (uint32_t)o < S ? e.y : kInf;
+            }
+        // mode 3: the pair-interleaved tables (symbols >= S: +inf)
+        constexpr bool kT3 = TM >= 1;  // pair tables (symbols pre-doubled)
+        constexpr bool kT4 = TM == 1 || TM == 3;  // ... read by four 64-bit moves
+        f32x32 TA[4];
+        f32x8 TB[4];
+        if constexpr (kT3) {
+#pragma unroll
+            for (int o = 0; o < (int)kPairSym; ++o) {
+                const bool ok = (uint32_t)o < S;
+                const uint32_t oc = ok ? (uint32_t)o : S - 1u;  // unconditional loads, then selects
+                const float2 e0 = m.tab[((size_t)(blk * S + oc) * SM + 0) * 64 + lane];
+                const float2 e1 = m.tab[((size_t)(blk * S + oc) * SM + 1) * 64 + lane];
+                const float4 h = *reinterpret_cast<const float4*>(m.hc + oc * 8);
+                // TM 3: {ea_0, ea_1}, {eb_0, eb_1}; otherwise {eb_0, ea_0}, {eb_1, ea_1}
+                const float2 t1 = TM >= 3 ? make_float2(e0.y, e1.y) : e0, t2 = TM >= 3 ? make_float2(e0.x, e1.x) : e1;
+                const float val[4][2] = {{ok ? t1.x : kInf, ok ? t1.y : kInf}, {ok ? t2.x : kInf, ok ? t2.y : kInf},
+                                         {ok ? h.x : kInf, ok ? h.y : kInf}, {ok ? h.z : kInf, ok ? h.w : kInf}};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int r = 2 * o + u;
+                        if (r < 32) TA[k][r] = val[k][u];
+                        else TB[k][r - 32] = val[k][u];
+                    }
+            }
+            // opaque per-lane values: the heavy constants are wave-uniform, and the compiler would
+            // otherwise keep them in SGPRs and copy them into the pinned registers at every step
+#pragma unroll
+            for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(TA[k]), "+v"(TB[k]));
+        }
+        // heavy constants as lane tables (lane o: symbol o), extracted with v_readlane
+        const bool lo = lane < S;
+        const float cAS = lo ? m.hc[lane * 8 + 0] : kInf, cAF = lo ? m.hc[lane * 8 + 1] : kInf;
+        const float cXSS = lo ? m.hc[lane * 8 + 2] : kInf, cXFF = lo ? m.hc[lane * 8 + 3] : kInf;
+        const float cXSF = lo ? m.hc[lane * 8 + 4] : kInf;
+        // ---- state at observation first-1
+        if (beg == 0) {
+            const uint32_t o0 = (uint32_t)uniform((int)sym[0]);
+#pragma unroll
+            for (int s = 0; s < SM; ++s) v[s] = m.e0[(size_t)o0 * P + p0 + s] + m.start[p0 + s];
+            CF.y = m.rowF >= 0 ? ctab[o0 * 8 + 5] + m.startF : kInf;
+            CF.x = (blk == 0 && lane == 0 && m.rowS >= 0) ? ctab[o0 * 8 + 6] + m.startS : kInf;
+        } else {
+            const float* vin = b.v_in + (size_t)b.v_in_row[q] * m.n;
+#pragma unroll
+            for (int s = 0; s < SM; ++s) {
+                const uint32_t r = m.lrow[p0 + s];
+                v[s] = r != kNoRow ? vin[r] : kInf;
+            }
+            CF.y = m.rowF >= 0 ? vin[m.rowF] : kInf;
+            CF.x = (blk == 0 && lane == 0 && m.rowS >= 0) ? vin[m.rowS] : kInf;
+        }
+
+        // ---- decoded paths: outputs and the per-slot tie masks
+        float* const pring_w = pring + w * 32 * kPRingStride;
+        uint32_t* const cmq = PATHS ? b.cmask + b.cmask_off[q] : nullptr;
+        float* const ckq = PATHS ? b.ckpt + b.ckpt_off[q] : nullptr;
+        float2* const precq = PATHS ? b.prec + b.prec_off[q] : nullptr;
+        float* const fckq = PATHS ? b.fck + b.fck_off[q] : nullptr;
+        const uint32_t wstride = m.nblk * SM * 64;  // mask words per 32 rows
+        auto store_masks = [&](uint32_t word, uint32_t rows) {  // rows 32*word .. +rows-1 are in macc
+#pragma unroll
+            for (int s = 0; s < SM; ++s)
+                cmq[(size_t)word * wstride + (blk * SM + s) * 64 + lane] = macc[s] << (32u - rows);
+        };
+        auto checkpoint = [&](uint32_t t) {  // t % kCkptEvery == 0: the light scores of t
+            float* d = ckq + (size_t)(t / kCkptEvery) * m.P + p0;
+            if constexpr (SM == 2) {
+                *reinterpret_cast<float2*>(d) = make_float2(v[0], v[1]);
+            } else {
+#pragma unroll
+                for (int s = 0; s < SM; ++s) d[s] = v[s];
+            }
+        };
+        auto ring_put2 = [&](uint32_t t) {  // {light minimum of t-1, sink partial of t}
+            *reinterpret_cast<float2*>(pring_w + (t & 31u) * kPRingStride + lane * 2) = make_float2(last_pm, CF.x);
+        };
+        // fold rows tb .. tb+31 of the ring (tb % 32 == 0) and store observations t in [1, thi):
+        // lane l reduces row l % 32 over the half-wave l / 32 (conflict-free: rows 528 B apart)
+        auto reduce_ring = [&](uint32_t tb, uint32_t thi) {
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const uint32_t R = lane & 31u, H = lane >> 5;
+            const float4* rp = reinterpret_cast<const float4*>(pring_w + R * kPRingStride + H * 64);
+            float mm = kInf, cc = kInf;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float4 e = rp[i];
+                mm = fminf(mm, fminf(e.x, e.z));
+                cc = fminf(cc, fminf(e.y, e.w));
+            }
+            const uint32_t tt = tb + R;
+            if (tt >= 1 && tt < thi) precq[((size_t)blk * 2 + H) * len + tt] = make_float2(mm, cc);
+        };
+        // after the step of observation t (compile-time positions in the unrolled body)
+        auto paths_after = [&](uint32_t t, auto maskc, auto ckc, auto redc) {
+            if constexpr (PATHS) {
+                ring_put2(t);
+                if constexpr (decltype(maskc)::value) {
+                    if (t >= 32) store_masks((t >> 5) - 1, 32);
+                    if (blk == 0 && lane == 0) fckq[t >> 5] = CF.y;
+                }
+                if constexpr (decltype(ckc)::value) checkpoint(t);
+                if constexpr (decltype(redc)::value) reduce_ring(t - 31, len);
+            }
+        };
+        auto paths_after_rt = [&](uint32_t t) {  // runtime positions (head / tail)
+            if constexpr (PATHS) {
+                ring_put2(t);
+                if ((t & 31u) == 0) {
+                    if (t >= 32) store_masks((t >> 5) - 1, 32);
+                    if (blk == 0 && lane == 0) fckq[t >> 5] = CF.y;
+                }
+                if ((t & (kCkptEvery - 1)) == 0) checkpoint(t);
+                if ((t & 31u) == 31u) reduce_ring(t - 31, len);
+            }
+        };
+        if constexpr (PATHS) {
+#pragma unroll
+            for (int s = 0; s < SM; ++s) {
+                const uint32_t f = m.pflags[p0 + s];
+                const bool ec = f & 1u, eaf = f & 2u, hl = f & 4u;
+                pmC[s] = __builtin_amdgcn_ballot_w64(eaf && (!ec || hl));
+            }
+            checkpoint(0);
+            if (blk == 0 && lane == 0) fckq[0] = CF.y;
+        }
+
+        // ---- symbols: 1024-observation windows in VGPRs (lane l: bytes 16l..16l+15)
+        const uint32_t slen = len + kSymPad;
+        // Observations run in groups of 32 aligned to `first` (tb = first % 32; 0 for the path
+        // variants, whose records sit at absolute multiples of 32): the body starts at first
+        // itself, with no head of single observations (each one an LDS or L2 round trip, and the
+        // head's cost adds up along the chain of waves).  What is indexed by the position in the
+        // cycle of 32 -- symbol windows, LDS ring slots -- uses u = t - tb; counts, granules and
+        // tags use t.
+#ifdef SVH_PIPE_HEAD  // A/B diagnostic: the head of single observations of before
+        const uint32_t tb = 0u;
+#else
+        const uint32_t tb = PATHS ? 0u : (first & 31u);
+#endif
+        auto load_window_raw = [&](uint32_t wi) -> uint4 {  // lane l: symbols of u = 1024 wi + 16 l ..
+            const uint32_t off = wi * kPipeWindow + lane * 16 + tb;
+            if ((tb & 15u) == 0)
+                return off < slen ? *reinterpret_cast<const uint4*>(sym + off) : make_uint4(0, 0, 0, 0);
+            // unaligned: two aligned 16-byte loads and a byte funnel shift (once per window)
+            const uint32_t a = off & ~15u, ws = (tb & 15u) >> 2, bs = tb & 3u;
+            const uint4 c0 = a < slen ? *reinterpret_cast<const uint4*>(sym + a) : make_uint4(0, 0, 0, 0);
+            const uint4 c1 = a + 16 < slen ? *reinterpret_cast<const uint4*>(sym + a + 16) : make_uint4(0, 0, 0, 0);
+            auto pick = [&](uint32_t i) -> uint32_t {  // word ws + i of c0 | c1 (selects, no scratch)
+                const uint32_t k = ws + i;
+                uint32_t r = c0.x;
+                r = k == 1 ? c0.y : r;
+                r = k == 2 ? c0.z : r;
+                r = k == 3 ? c0.w : r;
+                r = k == 4 ? c1.x : r;
+                r = k == 5 ? c1.y : r;
+                r = k == 6 ? c1.z : r;
+                r = k == 7 ? c1.w : r;
+                return r;
+            };
+            const uint32_t p0 = pick(0), p1 = pick(1), p2 = pick(2), p3 = pick(3), p4 = pick(4);
+            return make_uint4(__builtin_amdgcn_alignbyte(p1, p0, bs), __builtin_amdgcn_alignbyte(p2, p1, bs),
+                              __builtin_amdgcn_alignbyte(p3, p2, bs), __builtin_amdgcn_alignbyte(p4, p3, bs));
+        };
+        auto load_window = [&](uint32_t wi) -> uint4 {  // mode 3: every symbol byte doubled (2o < 64)
+            const uint4 w4 = load_window_raw(wi);
+            if constexpr (kT3) return make_uint4(w4.x << 1, w4.y << 1, w4.z << 1, w4.w << 1);
+            return w4;
+        };
+        uint32_t cwi = (first - tb) >> 10;
+        uint4 cw = load_window(cwi), nw = load_window(cwi + 1);
+        // The wait budget is per window: a new window resets a healthy counter (a give-up sticks),
+        // so no sequence length exhausts it while a stuck wait still gives up within one budget.
+        auto window_for = [&](uint32_t t) {  // uniform; windows advance one at a time
+            if (((t - tb) >> 10) != cwi) {
+                cw = nw;
+                ++cwi;
+                nw = load_window(cwi + 1);
+                spins = spins > kSpinLimit ? spins : 0u;
+            }
+        };
+        auto sym1 = [&](uint32_t t) -> uint32_t {  // symbol of observation t (slow path)
+            const uint32_t r = (t - tb) & 1023u, ln = r >> 4, d = (r >> 2) & 3u;
+            const uint32_t wd = d == 0 ? readlane_u(cw.x, ln) : d == 1 ? readlane_u(cw.y, ln)
+                              : d == 2 ? readlane_u(cw.z, ln) : readlane_u(cw.w, ln);
+            return (wd >> ((r & 3u) * 8)) & 0xFFu;
+        };
+
+        // ---- one observation with symbol o; bnd = the previous block's last score at t-1
+        // `in`: ChainIn<R>, slot 0's chain input (see ChainIn)
+        auto step = [&](uint32_t o, auto in) {
+            constexpr int R = decltype(in)::value;
+            float xa[SM], xb[SM];  // feeder and chain terms of every slot
+            if constexpr (TM == 2 || TM == 4) {  // o is 2 x the symbol: the table reads are indexed operands
+                // of the adds that use them (one gpr_idx(SRC0) block; only eb_0 is moved out, for
+                // slot 0's DPP chain add)
+                const float pm = fminf(v[0], v[1]);  // the heavy side reads the scores of t-1
+                f2 pmv;  // the packed add reads the low half twice (op_sel_hi): the high half is never read
+                pmv.x = pm;
+                float eb0;
+                f2 s1, s2;  // {A_S + m, A_F + m}, {X_SS + c, X_FF + F}
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+#pragma clang diagnostic ignored "-Wuninitialized"
+                if constexpr (TM == 2) {
+                asm("s_set_gpr_idx_on %[o], gpr_idx(SRC0)\n\t"
+                    "v_mov_b32 %[eb0], v2\n\t"
+                    "v_add_f32 %[xa0], v3, %[f]\n\t"
+                    "v_add_f32 %[xa1], v43, %[f]\n\t"
+                    "v_add_f32 %[xb1], v42, %[v0]\n\t"
+                    "v_pk_add_f32 %[s1], v[82:83], %[pm] op_sel_hi:[1,0]\n\t"
+                    "v_pk_add_f32 %[s2], v[122:123], %[cf]\n\t"
+                    "s_set_gpr_idx_off"
+                    : [eb0] "=&v"(eb0), [xa0] "=&v"(xa[0]), [xa1] "=&v"(xa[1]), [xb1] "=&v"(xb[1]), [s1] "=&v"(s1),
+                      [s2] "=&v"(s2)
+                    : [o] "s"(o), [f] "v"(CF.y), [v0] "v"(v[0]), [pm] "v"(pmv), [cf] "v"(CF), "{v[2:33]}"(TA[0]),
+                      "{v[34:41]}"(TB[0]), "{v[42:73]}"(TA[1]), "{v[74:81]}"(TB[1]), "{v[82:113]}"(TA[2]),
+                      "{v[114:121]}"(TB[2]), "{v[122:153]}"(TA[3]), "{v[154:161]}"(TB[3])
+                    : "m0");
+                } else {  // T1 = {ea_0, ea_1}: one packed feeder add, F from the high half of CF
+                f2 xap;
+                asm("s_set_gpr_idx_on %[o], gpr_idx(SRC0)\n\t"
+                    "v_mov_b32 %[eb0], v42\n\t"
+                    "v_pk_add_f32 %[xa], v[2:3], %[cf] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+                    "v_add_f32 %[xb1], v43, %[v0]\n\t"
+                    "v_pk_add_f32 %[s1], v[82:83], %[pm] op_sel_hi:[1,0]\n\t"
+                    "v_pk_add_f32 %[s2], v[122:123], %[cf]\n\t"
+                    "s_set_gpr_idx_off"
+                    : [eb0] "=&v"(eb0), [xa] "=&v"(xap), [xb1] "=&v"(xb[1]), [s1] "=&v"(s1), [s2] "=&v"(s2)
+                    : [o] "s"(o), [v0] "v"(v[0]), [pm] "v"(pmv), [cf] "v"(CF), "{v[2:33]}"(TA[0]),
+                      "{v[34:41]}"(TB[0]), "{v[42:73]}"(TA[1]), "{v[74:81]}"(TB[1]), "{v[82:113]}"(TA[2]),
+                      "{v[114:121]}"(TB[2]), "{v[122:153]}"(TA[3]), "{v[154:161]}"(TB[3])
+                    : "m0");
+                xa[0] = xap.x;
+                xa[1] = xap.y;
+                }
+#pragma clang diagnostic pop
+                xb[0] = chain_b<R>(eb0, in.b, v[1]);
+                float cn = fminf(s1.x, s2.x);
+                if constexpr (SX) cn = fminf(cn, readlane_f(cXSF, o >> 1) + CF.y);
+                asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+                             : "+v"(viol)
+                             : "v"(s1.y), "v"(s2.y)
+                             : "vcc");
+                auto push = [&](int s, float a, float bb) {
+                    if constexpr (PATHS == 2) push_le(macc[s], a, bb);
+                    else if constexpr (PATHS == 1) push_lt_eqc(macc[s], a, bb, pmC[s]);
+                };
+                if constexpr (PATHS) last_pm = pm;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    if constexpr (PATHS) push(s, xa[s], xb[s]);
+                    v[s] = fminf(xa[s], xb[s]);
+                }
+                CF = (f2){cn, s2.y};
+                return;
+            } else if constexpr (kT4) {  // o is 2 x the symbol: four 64-bit moves out of the pair tables
+                f2 p0, p1, kS, kX;  // {eb_0, ea_0}, {eb_1, ea_1}, {A_S, A_F}, {X_SS, X_FF}
+                // M0 is reserved (clang warns on the clobber); the kernel uses it nowhere else
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+                asm("s_set_gpr_idx_on %[o], gpr_idx(SRC0)\n\t"
+                    "v_mov_b64 %[p0], v[2:3]\n\t"
+                    "v_mov_b64 %[p1], v[42:43]\n\t"
+                    "v_mov_b64 %[ks], v[82:83]\n\t"
+                    "v_mov_b64 %[kx], v[122:123]\n\t"
+                    "s_set_gpr_idx_off"
+                    : [p0] "=&v"(p0), [p1] "=&v"(p1), [ks] "=&v"(kS), [kx] "=&v"(kX)
+                    : [o] "s"(o), "{v[2:33]}"(TA[0]), "{v[34:41]}"(TB[0]), "{v[42:73]}"(TA[1]), "{v[74:81]}"(TB[1]),
+                      "{v[82:113]}"(TA[2]), "{v[114:121]}"(TB[2]), "{v[122:153]}"(TA[3]), "{v[154:161]}"(TB[3])
+                    : "m0");
+#pragma clang diagnostic pop
+                if constexpr (TM == 3) {  // p0 = {ea_0, ea_1}, p1 = {eb_0, eb_1}
+                    f2 xap;
+                    chain_terms_pk<R>(xb[0], xap, p0, p1.x, in.b, CF, v[1]);
+                    xa[0] = xap.x;
+                    xa[1] = xap.y;
+                    xb[1] = p1.y + v[0];
+                } else {
+                    if constexpr (R < 0) chain_terms(xb[0], xa[0], p0.x, p0.y, in.b, CF.y, v[1]);
+                    else chain_terms_v<R>(xb[0], xa[0], p0.x, p0.y, in.b, CF.y, v[1]);
+                    xa[1] = p1.y + CF.y;
+                    xb[1] = p1.x + v[0];
+                }
+                const float pm = fminf(v[0], v[1]);
+                const f2 s1 = kS + (f2){pm, pm};  // A_S + m, A_F + m
+                const f2 s2 = kX + CF;            // X_SS + c, X_FF + F
+                float cn = fminf(s1.x, s2.x);
+                if constexpr (SX) cn = fminf(cn, readlane_f(cXSF, o >> 1) + CF.y);
+                asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+                             : "+v"(viol)
+                             : "v"(s1.y), "v"(s2.y)
+                             : "vcc");
+                auto push = [&](int s, float a, float bb) {
+                    if constexpr (PATHS == 2) push_le(macc[s], a, bb);
+                    else if constexpr (PATHS == 1) push_lt_eqc(macc[s], a, bb, pmC[s]);
+                };
+                if constexpr (PATHS) last_pm = pm;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    if constexpr (PATHS) push(s, xa[s], xb[s]);
+                    v[s] = fminf(xa[s], xb[s]);
+                }
+                CF = (f2){cn, s2.y};
+                return;
+            }
+            const float kas = readlane_f(cAS, o), kaf = readlane_f(cAF, o);
+            const float kxss = readlane_f(cXSS, o), kxff = readlane_f(cXFF, o);
+            {
+                float eb[SM], ea[SM];
+#pragma unroll
+                for (int s = 0; s < SM; ++s) {
+                    eb[s] = EB[s][o];
+                    ea[s] = EA[s][o];
+                }
+#pragma unroll
+                for (int s = 0; s < SM; ++s) asm volatile("" : "+v"(eb[s]), "+v"(ea[s]));  // one idx block
+                if constexpr (R < 0) chain_terms(xb[0], xa[0], eb[0], ea[0], in.b, CF.y, v[SM - 1]);
+                else chain_terms_v<R>(xb[0], xa[0], eb[0], ea[0], in.b, CF.y, v[SM - 1]);
+#pragma unroll
+                for (int s = 1; s < SM; ++s) {
+                    xa[s] = ea[s] + CF.y;
+                    xb[s] = eb[s] + v[s - 1];
+                }
+            }
+            float vn[SM];
+            auto push = [&](int s, float a, float bb) {  // PATHS: F's term taken (row t-1's bit)
+                if constexpr (PATHS == 2) push_le(macc[s], a, bb);
+                else if constexpr (PATHS == 1) push_lt_eqc(macc[s], a, bb, pmC[s]);
+            };
+#pragma unroll
+            for (int s = 0; s < SM; ++s) {
+                vn[s] = fminf(xa[s], xb[s]);
+                if constexpr (PATHS) push(s, xa[s], xb[s]);
+            }
+            // heavy side from the scores of t-1
+            float pm = v[0];
+#pragma unroll
+            for (int s = 1; s < SM; ++s) pm = fminf(pm, v[s]);
+            if constexpr (PATHS) last_pm = pm;
+            const f2 s1 = (f2){kas, kaf} + (f2){pm, pm};  // A_S + m, A_F + m
+            const f2 s2 = (f2){kxss, kxff} + CF;          // X_SS + c, X_FF + F
+            float cn = fminf(s1.x, s2.x);
+            if constexpr (SX) cn = fminf(cn, readlane_f(cXSF, o) + CF.y);
+            // viol += [A_F + m < F'] per lane: compare into VCC, add with carry-in (two VALU, no
+            // VALU -> SALU dependency per step)
+            asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+                         : "+v"(viol)
+                         : "v"(s1.y), "v"(s2.y)
+                         : "vcc");
+            CF = (f2){cn, s2.y};
+#pragma unroll
+            for (int s = 0; s < SM; ++s) v[s] = vn[s];
+        };
+
+        // ---- exchange state
+        float* const ring_w = ring + w * kR * 64;
+        const float* const ring_prev = ring_w - kR * 64;
+        uint32_t* const cnt_w = cnt + w;
+        const uint32_t cnt_addr = lds_addr(cnt_w);
+        // SVH_PIPE_PUT 1: lane 0 -> the count, lane l > 0 -> sink[w][l]
+        const uint32_t cnt_vaddr = lane == 0 ? cnt_addr : lds_addr(tick + 4 + (w * 64 + lane));
+        auto put_cnt = [&](uint32_t val) {
+            if constexpr (SVH_PIPE_PUT) lds_put_v(cnt_vaddr, val);
+            else lds_put1(cnt_addr, val);
+        };
+        uint64_t* const gin = x.gran + ((size_t)q * (G - 1) + (g - 1)) * kGR;  // src == 2
+        uint64_t* const gout = x.gran + ((size_t)q * (G - 1) + g) * kGR;       // dst == 2
+        uint64_t* const cons_in = reinterpret_cast<uint64_t*>(x.cons) + (size_t)q * G + g;      // src == 2 publishes
+        const uint64_t* const cons_out = reinterpret_cast<const uint64_t*>(x.cons) + (size_t)q * G + g + 1;  // dst == 2 reads
+        float bprev = kInf;  // boundary score of observation t-1 for the next step (uniform)
+
+        auto give_up = [&]() -> bool { return ++spins > kSpinLimit; };
+        // SVH_PIPE_XL: is workgroup og of this row on this wave's XCD?  (bounded poll of its id; not
+        // known in time: no, i.e. write-through stores, always correct)
+        auto xcc_local = [&](uint32_t og) -> bool {
+#if SVH_PIPE_XL
+            if (!x.xcc) return false;
+            const uint32_t* p = x.xcc + (size_t)q * G + og;
+            for (int i = 0; i < 32; ++i) {
+                const uint32_t wv = (uint32_t)uniform((int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if ((wv >> 4) == (ep & 0x0FFFFFFFu)) return (wv & 0xFu) == my_xcc;
+                __builtin_amdgcn_s_sleep(4);
+            }
+#endif
+            (void)og;
+            return false;
+        };
+        bool gran_plain = false, cons_plain = false;
+        // granule / progress-word stores: plain when the reader shares this XCD (SVH_PIPE_XL)
+        auto st_gran = [&](uint64_t* a, uint64_t v64) {
+            if (SVH_PIPE_XL && gran_plain) *a = v64;
+            else g_st64(a, v64);
+        };
+        auto st_cons = [&](uint64_t v64) {
+            if (SVH_PIPE_XL && cons_plain) *cons_in = v64;
+            else g_st64(cons_in, v64);
+        };
+        // wait until the previous wave has published observations < need
+        auto wait_prev = [&](uint32_t need) {
+            while ((uint32_t)uniform((int)lds_ld32(cnt_w - 1)) < need) {
+                if (dbg) ++dg[3];
+                if (give_up()) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        };
+        // flow control: the next wave has consumed observations < need
+        auto wait_next = [&](uint32_t need) {
+            while ((int)uniform((int)lds_ld32(cnt_w + 1)) < (int)need) {
+                if (dbg) ++dg[4];
+                if (give_up()) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        };
+        // The boundary score of observation s from the previous workgroup's granules (uniform), for
+        // the single observations (the tail, the path variants' head): eight granules per poll
+        // (lanes 0..7: s .. s+7), one L2 round trip per 8 observations instead of one each.
+        // Only granules this wave reads (observations <= len-2) are awaited.
+        float gvec = 0.0f;
+        uint32_t gbase = 0x80000000u;  // no observation index reaches it: the first call loads
+        auto gran_single = [&](uint32_t s) -> float {
+            if (s - gbase >= 8u) {
+                gbase = s;
+                const uint32_t sl = s + (lane & 7u);
+                const bool need = lane < 8u && sl + 1u < len;
+                const uint64_t* p = gin + (sl & (kGR - 1));
+                uint64_t gv = g_ld64(p);
+                while (__builtin_amdgcn_ballot_w64(need && (uint32_t)(gv >> 32) != gtag(ep, sl)) != 0) {
+                    if (dbg) ++dg[5];
+                    if (give_up()) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    gv = g_ld64(p);
+                }
+                gvec = __builtin_bit_cast(float, (uint32_t)gv);
+            }
+            return readlane_f(gvec, s - gbase);
+        };
+        auto cons_ok = [&](uint64_t c, uint32_t need) -> bool {  // consumer progress word vs need
+            return (uint32_t)(c >> 32) == ep && (int)(uint32_t)c >= (int)need;
+        };
+        auto uni64 = [](uint64_t c) -> uint64_t {
+            return (uint64_t)(uint32_t)uniform((int)(uint32_t)c) | ((uint64_t)(uint32_t)uniform((int)(uint32_t)(c >> 32)) << 32);
+        };
+        auto wait_cons = [&](uint32_t need) {
+            uint64_t c = g_ld64(cons_out);
+            while (!cons_ok(uni64(c), need)) {
+                if (dbg) ++dg[6];
+                if (give_up()) break;
+                __builtin_amdgcn_s_sleep(2);
+                c = g_ld64(cons_out);
+            }
+        };
+        auto put_gran1 = [&](uint32_t s, float val) {  // single observation (slow path), lane 0 stores
+            const uint64_t gv = ((uint64_t)gtag(ep, s) << 32) | __builtin_bit_cast(uint32_t, val);
+            if (lane == 0) g_st64(gout + (s & (kGR - 1)), gv);
+        };
+        auto ring_put = [&](uint32_t t, float val) { ring_w[ring_idx((t - tb) & (kR - 1), lane)] = val; };
+
+        // The sweep, with the boundary roles as compile-time constants (one code path per role).
+        auto sweep = [&](auto srcc, auto dstc) {
+            constexpr int SRC = decltype(srcc)::value, DST = decltype(dstc)::value;
+            // one observation outside the unrolled groups: per-observation waits
+            auto single = [&](uint32_t t) {
+                window_for(t);
+                const uint32_t o = (uint32_t)uniform((int)sym1(t));
+                if constexpr (DST == 1) wait_next((int)t - (int)kR + 1);
+                if constexpr (DST == 2) {
+                    if ((t & 63u) == 0) wait_cons((int)t - (int)kGR + 64);
+                }
+                step(o, ChainIn<-1>{bprev});
+                ring_put(t, v[SM - 1]);
+                if constexpr (DST == 2) put_gran1(t, readlane_f(v[SM - 1], 63));
+                paths_after_rt(t);
+                if (t + 1 < len) {  // fetch the boundary score of t for the next step
+                    if constexpr (SRC == 1) {
+                        wait_prev(t + 1);
+                        asm volatile("" ::: "memory");
+                        bprev = readlane_f(ring_prev[ring_idx((t - tb) & (kR - 1), 63)], 0);
+                    } else if constexpr (SRC == 2) {
+                        bprev = gran_single(t);
+                    }
+                }
+                asm volatile("" ::: "memory");
+                put_cnt(t + 1);
+                if constexpr (SRC == 2) {
+                    if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | (t + 1));
+                }
+            };
+
+            if constexpr (SVH_PIPE_XL && DST == 2) gran_plain = xcc_local(g + 1);
+            if constexpr (SVH_PIPE_XL && SRC == 2) cons_plain = xcc_local(g - 1);
+            // publish the state at first-1 and fetch the boundary of first-1
+            ring_put(first - 1, v[SM - 1]);
+            if constexpr (DST == 2) put_gran1(first - 1, readlane_f(v[SM - 1], 63));
+            asm volatile("" ::: "memory");
+            put_cnt(first);
+            if constexpr (SRC == 1) {
+                wait_prev(first);
+                asm volatile("" ::: "memory");
+                bprev = readlane_f(ring_prev[ring_idx((first - 1 - tb) & (kR - 1), 63)], 0);
+            } else if constexpr (SRC == 2) {
+                // initial progress (observations < first are done), published before the first
+                // poll: a row that starts mid-sequence at a multiple of 64 would otherwise leave its
+                // producer's first flow-control wait on a stale word while this wave waits for that
+                // producer's granules (the poll awaits observations up to first+6)
+                if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | first);
+                bprev = gran_single(first - 1);
+            }
+
+            uint32_t t = first;
+            unsigned long long c0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+            SVH_RT(9);
+            // head: single observations up to the first group of 32 (none unless tb is forced to 0)
+            for (; t < len && ((t - tb) & 31u); ++t) single(t);
+            if (dbg) {
+                const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+                dg[1] = c1 - c0;
+                c0 = c1;
+            }
+
+            // body: 32 observations per iteration, four groups of 8
+            if (t + 32 <= len) {
+                uint64_t gq[kGpf] = {};  // SRC 2: granule groups in flight
+                // SRC 2 waves whose only body stores are the progress words (see SVH_PIPE_VMS)
+                constexpr bool kVmStore = SVH_PIPE_VMS && SRC == 2 && DST != 2 && PATHS == 0 && kGpf == 2;
+                if constexpr (SRC == 2) {
+#pragma unroll
+                    for (uint32_t j = 0; j < kGpf; ++j) g_prefetch64(gq[j], gin + ((t + kG * j + (lane & (kG - 1))) & (kGR - 1)));
+                    // store-aware counts: the first iteration's first two groups also find one store
+                    // queued behind their prefetches (the progress word again: observations < t done)
+                    if constexpr (kVmStore) {
+                        if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | t);
+                    }
+                }
+                float gpend = 0.0f;    // DST 2: the previous group's boundary scores (lanes 0..7),
+                uint32_t gpend_t = 0;  // read back from the ring one group before they are stored
+                uint64_t cons_v = 0;   // DST 2: prefetched progress word of the consumer
+                if constexpr (DST == 2) cons_v = g_ld64(cons_out);
+                // counts of the neighbouring waves, read two observations before the end of a group
+                uint32_t pc_rd = 0, nc_rd = 0;
+                if constexpr (DST == 1) nc_rd = lds_ld32(cnt_w + 1);
+                // boundary vectors (lanes 0..7 = the previous block's last scores of a group's 8
+                // observations): the previous group's (lane 7 feeds the first step) and, SRC 1,
+                // the next group's, read one group ahead whenever the producer is far enough
+                float bv_prev = bprev;  // lane 7 (all lanes) = boundary of t-1
+                // SRC 1: the next group's vector, loaded at the end of every group (stale unless
+                // next_ok) into this one loop-carried register, re-loaded there when it was stale
+                float bv_next = kInf;
+                bool next_ok = false;
+                if constexpr (SRC == 1) bv_next = ring_prev[ring_idx(((t - tb) & (kR - 1)) + (lane & (kG - 1)), 63)];  // group at t
+                while (t + 32 <= len) {
+                  // the window of t, loaded and waited for here (an asm use), so no load of it is
+                  // pending inside the iterations: the compiler would otherwise wait for every
+                  // vector-memory operation (granule prefetches and stores included) before each
+                  // iteration's reads of the window
+                  cwi = (t - tb) >> 10;
+                  cw = load_window(cwi);
+                  asm volatile("" ::"v"(cw.x), "v"(cw.y), "v"(cw.z), "v"(cw.w));
+                  spins = spins > kSpinLimit ? spins : 0u;  // new window, new budget (a give-up sticks)
+                  const uint32_t wend = ((cwi + 1) << 10) + tb;
+                  for (; t + 32 <= len && t < wend; t += 32) {
+                    if (dbg) ++dg[7];
+                    const uint32_t r = (t - tb) & 1023u, ln = r >> 4;
+                    const uint32_t ub = (t - tb) & (kR - 1);  // G16: ring position of t (0 or 32)
+                    const uint64_t sw0 = (uint64_t)readlane_u(cw.x, ln) | ((uint64_t)readlane_u(cw.y, ln) << 32);
+                    const uint64_t sw1 = (uint64_t)readlane_u(cw.z, ln) | ((uint64_t)readlane_u(cw.w, ln) << 32);
+                    const uint64_t sw2 = (uint64_t)readlane_u(cw.x, ln + 1) | ((uint64_t)readlane_u(cw.y, ln + 1) << 32);
+                    const uint64_t sw3 = (uint64_t)readlane_u(cw.z, ln + 1) | ((uint64_t)readlane_u(cw.w, ln + 1) << 32);
+                    if constexpr (DST == 2) {  // granule ring flow control, once per 32 observations
+                        if (!cons_ok(uni64(cons_v), (int)t + 32 - (int)kGR + (int)kG)) wait_cons((int)t + 32 - (int)kGR + (int)kG);
+                        cons_v = g_ld64(cons_out);
+                    }
+                    auto group = [&](auto jc, uint64_t swl, uint64_t swh) {
+                        constexpr uint32_t j = decltype(jc)::value;
+                        const uint32_t tg = t + kG * j;
+                        float bv = kInf;  // lanes 0..7: the previous block's last scores of tg..tg+7
+                        float gl[kG];     // SVH_PIPE_RING8: this group's last-slot scores
+                        if constexpr (SRC == 2) {
+                            // gq[j]: kGpf - 1 later loads in flight (+ the progress store, groups 0, 1)
+                            if constexpr (kVmStore && j < 1) wait_vmcnt<kGpf>();
+                            else wait_vmcnt<kGpf - 1>();
+                            uint64_t gv = gq[j % kGpf];
+                            while (__builtin_amdgcn_ballot_w64((uint32_t)(gv >> 32) != gtag(ep, tg)) != 0) {
+                                if (dbg) ++dg[5];
+                                if (give_up()) break;
+                                __builtin_amdgcn_s_sleep(1);
+                                gv = g_ld64(gin + ((tg + (lane & (kG - 1))) & (kGR - 1)));
+                            }
+                            bv = __builtin_bit_cast(float, (uint32_t)gv);
+                            g_prefetch64(gq[j % kGpf], gin + ((tg + kG * kGpf + (lane & (kG - 1))) & (kGR - 1)));
+                        }
+                        if constexpr (DST == 1) {
+                            if constexpr (SVH_PIPE_LDSX) asm volatile("" : "+v"(nc_rd));
+                            if ((int)uniform((int)nc_rd) < (int)tg + (int)kG - (int)kR) wait_next((int)tg + (int)kG - (int)kR);
+                        }
+                        auto one = [&](auto kc) {
+                            constexpr uint32_t k = decltype(kc)::value;
+                            const uint32_t o = (uint32_t)(((k < 8 ? swl : swh) >> (8 * (k & 7u))) & 0xFFu);
+                            if constexpr (SRC == 1 && k == 1) {  // step 0 used only the previous vector
+                                if (!next_ok) {  // the producer had not published this group: wait, re-load
+                                    wait_prev(tg + kG);
+                                    asm volatile("" ::: "memory");
+                                    uint32_t z = 0;  // SVH_PIPE_LDSX: an address the compiler cannot hoist
+                                    if constexpr (SVH_PIPE_LDSX) asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                                    bv_next = ring_prev[ring_idx(ub + kG * j + (lane & (kG - 1)), 63) + z];
+                                }
+                            }
+                            if constexpr (SRC == 1) bv = bv_next;
+                            if constexpr (k == 0) {
+                                step(o, ChainIn<(int)kG - 1>{bv_prev});
+                            } else {
+                                step(o, ChainIn<(int)k - 1>{bv});
+                            }
+                            if constexpr (SVH_PIPE_RING8) {  // kept for the group's two 16-byte stores
+                                gl[k] = v[SM - 1];
+                                if constexpr (k % 4 == 3)
+                                    *reinterpret_cast<float4*>(ring_w + ring_idx(ub + kG * j + k - 3, lane)) =
+                                        make_float4(gl[k - 3], gl[k - 2], gl[k - 1], gl[k]);
+                            } else {
+                                ring_w[ring_idx(ub + kG * j + k, lane)] = v[SM - 1];
+                            }
+                            if constexpr (k == kGcnt) {  // the counts checked at the end of the group
+                                asm volatile("" ::: "memory");
+                                if constexpr (SRC == 1) pc_rd = lds_ld32(cnt_w - 1);
+                                if constexpr (DST == 1) nc_rd = lds_ld32(cnt_w + 1);
+                                // SVH_PIPE_LDSX: issued here, not where the scheduler would sink them (the
+                                // group's end, right before their use)
+                                if constexpr (SVH_PIPE_LDSX) __builtin_amdgcn_sched_barrier(0);
+                            }
+                            if constexpr (SVH_PIPE_LDSX && SVH_PIPE_RING8 && k == kGcnt - 1) __builtin_amdgcn_sched_barrier(0);
+                            if constexpr (DST == 2 && kGst != 0 && k == kGst) {  // the last group's granules
+                                if (gpend_t && lane < kG)
+                                    st_gran(gout + ((gpend_t + lane) & (kGR - 1)),
+                                           ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
+                                gpend_t = 0;
+                            }
+                        };
+                        one(std::integral_constant<uint32_t, 0>{});
+                        one(std::integral_constant<uint32_t, 1>{});
+                        one(std::integral_constant<uint32_t, 2>{});
+                        one(std::integral_constant<uint32_t, 3>{});
+                        one(std::integral_constant<uint32_t, 4>{});
+                        one(std::integral_constant<uint32_t, 5>{});
+                        one(std::integral_constant<uint32_t, 6>{});
+                        one(std::integral_constant<uint32_t, 7>{});
+                        one(std::integral_constant<uint32_t, 8>{});
+                        one(std::integral_constant<uint32_t, 9>{});
+                        one(std::integral_constant<uint32_t, 10>{});
+                        one(std::integral_constant<uint32_t, 11>{});
+                        one(std::integral_constant<uint32_t, 12>{});
+                        one(std::integral_constant<uint32_t, 13>{});
+                        one(std::integral_constant<uint32_t, 14>{});
+                        one(std::integral_constant<uint32_t, 15>{});
+                        bv_prev = bv;
+                        asm volatile("" ::: "memory");
+                        put_cnt(tg + kG);
+                        if constexpr (SRC == 1) {  // the next group's boundary vector (valid if next_ok)
+                            if constexpr (SVH_PIPE_LDSX) asm volatile("" : "+v"(pc_rd));
+                            next_ok = (uint32_t)uniform((int)pc_rd) >= tg + 2 * kG;
+                            asm volatile("" ::: "memory");
+                            bv_next = ring_prev[ring_idx(((ub + kG * j + kG) & (kR - 1)) + (lane & (kG - 1)), 63)];
+                        }
+                        if constexpr (DST == 2) {
+                            // granules of the previous group (read back from the ring one group ago)
+                            if constexpr (kGst == 0) {
+                                if (gpend_t && lane < kG)
+                                    st_gran(gout + ((gpend_t + lane) & (kGR - 1)),
+                                           ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
+                            }
+                            gpend = ring_w[ring_idx(ub + kG * j + (lane & (kG - 1)), 63)];
+                            gpend_t = tg;
+                        }
+                        if constexpr (SRC == 2 && j == 32 / kG - 1) {
+                            if (lane == 0) st_cons(((uint64_t)ep << 32) | (tg + kG));
+                        }
+                    };
+                    group(std::integral_constant<uint32_t, 0>{}, sw0, sw1);
+                    group(std::integral_constant<uint32_t, 1>{}, sw2, sw3);
+                  }
+                }
+                // the tail's windows; the tail's granule polls start afresh (nothing of the head's
+                // stays live through the body)
+                gbase = 0x80000000u;
+                cwi = (t - tb) >> 10;
+                cw = load_window(cwi);
+                nw = load_window(cwi + 1);
+                bprev = readlane_f(bv_prev, kG - 1);
+                if constexpr (SRC == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the prefetches
+                if constexpr (DST == 2) {
+                    if (gpend_t && lane < kG)
+                        st_gran(gout + ((gpend_t + lane) & (kGR - 1)),
+                               ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
+                }
+            }
+            if (dbg) {
+                const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+                dg[0] = c1 - c0;
+                c0 = c1;
+            }
+            SVH_RT(10);
+            // tail
+            for (; t < len; ++t) single(t);
+            if (dbg) dg[2] = __builtin_amdgcn_s_memtime() - c0;
+            SVH_RT(11);
+            if constexpr (PATHS) {
+                // rows the loop did not store: masks of rows below len-1 past the last full word,
+                // ring rows of the last partial group of 32
+                const uint32_t mdone = (len - 1) & ~31u;
+                if (mdone < len - 1) store_masks(mdone >> 5, len - 1 - mdone);
+                if (((len - 1) & 31u) != 31u) reduce_ring((len - 1) & ~31u, len);
+            }
+        };
+
+        if (len > first && dbg && (m.diag & 1u)) {
+            sweep(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});  // no exchange (timing only)
+        } else if (len > first) {
+            using I0 = std::integral_constant<int, 0>;
+            using I1 = std::integral_constant<int, 1>;
+            using I2 = std::integral_constant<int, 2>;
+            switch (src * 3 + dst) {
+                case 0: sweep(I0{}, I0{}); break;
+                case 1: sweep(I0{}, I1{}); break;
+                case 2: sweep(I0{}, I2{}); break;
+                case 3: sweep(I1{}, I0{}); break;
+                case 4: sweep(I1{}, I1{}); break;
+                case 5: sweep(I1{}, I2{}); break;
+                case 6: sweep(I2{}, I0{}); break;
+                case 7: sweep(I2{}, I1{}); break;
+                default: sweep(I2{}, I2{}); break;
+            }
+        }
+        if (dbg && lane == 0)
+            for (int k = 0; k < kPipeStamps; ++k) m.stamps[((size_t)id * W + w) * kPipeStamps + k] = dg[k];
+        if (spins > kSpinLimit && lane == 0 && b.fault) atomicOr(b.fault, kFaultPipe);
+
+        // ---- scores of the light positions and this wave's partials
+        float* out = b.scores + (size_t)q * m.n;
+        float bvv = kInf;
+        uint32_t bk = kNoRow;
+#pragma unroll
+        for (int s = 0; s < SM; ++s) {
+            const uint32_t r = m.lrow[p0 + s];
+            if (r != kNoRow) {
+                out[r] = v[s];
+                lex_min(bvv, bk, v[s], r);
+            }
+        }
+        wave_lexmin63(bvv, bk);
+        const float cmin = wave_min63(CF.x);
+        const bool any_viol = __builtin_amdgcn_ballot_w64(viol != 0) != 0;  // all lanes active here
+        if (lane == 63) {
+            red[w * 4 + 0] = cmin;
+            red[w * 4 + 1] = bvv;
+            red[w * 4 + 2] = __builtin_bit_cast(float, bk);
+            red[w * 4 + 3] = __builtin_bit_cast(float, any_viol ? 1u : 0u);
+        }
+    } else if (lane == 63) {
+        red[w * 4 + 0] = kInf;
+        red[w * 4 + 1] = kInf;
+        red[w * 4 + 2] = __builtin_bit_cast(float, kNoRow);
+        red[w * 4 + 3] = 0.0f;
+    }
+    __syncthreads();
+
+    // ---- per-sequence combine (the workgroup that finishes the sequence last) and launch end
+    if (tid == 0) {
+        float cm = kInf, bvv = kInf;
+        uint32_t bk = kNoRow, vi = 0;
+        for (uint32_t u = 0; u < (uint32_t)W; ++u) {
+            cm = fminf(cm, red[u * 4 + 0]);
+            lex_min(bvv, bk, red[u * 4 + 1], __builtin_bit_cast(uint32_t, red[u * 4 + 2]));
+            vi |= __builtin_bit_cast(uint32_t, red[u * 4 + 3]);
+        }
+        uint64_t* part = x.part + ((size_t)q * G + g) * 2;
+        g_st64(part, ((uint64_t)vi << 32) | __builtin_bit_cast(uint32_t, cm));
+        g_st64(part + 1, lex_key(bvv, bk));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t d = __hip_atomic_fetch_add(x.done + q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == G - 1) {
+            float C = kInf;
+            uint64_t key = ~0ull;
+            vi = 0;
+            for (uint32_t u = 0; u < G; ++u) {
+                const uint64_t* pu = x.part + ((size_t)q * G + u) * 2;
+                const uint64_t a = g_ld64(pu), k2 = g_ld64(pu + 1);
+                C = fminf(C, __builtin_bit_cast(float, (uint32_t)a));
+                vi |= (uint32_t)(a >> 32);
+                key = k2 < key ? k2 : key;
+            }
+            float* out = b.scores + (size_t)q * m.n;
+            float bv2 = lex_key_value(key);
+            uint32_t bk2 = lex_key_index(key);
+            if (key == ~0ull) {
+                bv2 = kInf;
+                bk2 = kNoRow;
+            }
+            if (m.rowF >= 0) {
+                out[m.rowF] = CF.y;
+                lex_min(bv2, bk2, CF.y, (uint32_t)m.rowF);
+            }
+            if (m.rowS >= 0) {
+                out[m.rowS] = C;
+                lex_min(bv2, bk2, C, (uint32_t)m.rowS);
+            }
+            if (b.best) b.best[q] = bk2 == kNoRow ? -1 : (int64_t)bk2;
+            x.viol[q] = vi;
+            __hip_atomic_store(x.done + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint32_t f = __hip_atomic_fetch_add(x.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (f == gridDim.x - 1) {  // every workgroup has taken its ticket and read the epoch
+            __hip_atomic_store(x.ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(x.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(x.ctr + 2, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+}  // namespace
+
+// The kernel's instantiations live in three translation units (they compile in parallel):
+// pipe.hip TM = 0 (every geometry, decoded-path variants at 2 x 4), pipe_tm1.hip TM = 1..4 (2 slots,
+// 4 waves), pipe_tm1p.hip TM = 1 / 4 decoded-path variants (2 x 4).  Each returns the kernel for
+// (slots, waves, sx, PATHS, ties_heavy) or nullptr.
+const void* pipe_kernel_tm0(int sm, int waves, bool sx, int paths);
+const void* pipe_kernel_tm1(int sm, int waves, bool sx, int paths);
+const void* pipe_kernel_tm1_paths(int sm, int waves, bool sx, int paths, int tm);
+
+}  // namespace svh

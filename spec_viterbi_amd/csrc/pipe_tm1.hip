@@ -8,7 +8,11 @@
 #ifndef SVH_PIPE_RING8
 #define SVH_PIPE_RING8 1
 #endif
+#ifdef SVH_PIPE_G16  // A/B experiment: groups of 16 observations (pipe_kernel_g16.h)
+#include "pipe_kernel_g16.h"
+#else
 #include "pipe_kernel.h"
+#endif
 
 namespace svh {
 
