@@ -55,7 +55,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t kR = 64;  // G16: four groups of 16 in the ring
 constexpr uint32_t kG = 16;
 #ifndef SVH_PIPE_G16_CNT
-#define SVH_PIPE_G16_CNT 8
+#define SVH_PIPE_G16_CNT 12  // measured best of 4, 8, 12, 14, 15
 #endif
 constexpr uint32_t kGcnt = SVH_PIPE_G16_CNT;  // step of the group at which the neighbours' counts are read
 
