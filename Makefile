@@ -17,7 +17,8 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) \
 HOSTFLAGS := --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall
 
 HIP_SRCS  := $(wildcard $(CSRC)/fused_*.hip) $(CSRC)/misc.hip $(CSRC)/band.hip $(wildcard $(CSRC)/chain_*.hip) $(CSRC)/timepar.hip $(CSRC)/pipe.hip \
-             $(CSRC)/pipe_tm1.hip $(CSRC)/pipe_tm1p.hip $(CSRC)/pipe_wide.hip $(CSRC)/pipe_wide_paths.hip $(CSRC)/pipe_paths.hip
+             $(CSRC)/pipe_tm1.hip $(CSRC)/pipe_tm1p.hip $(CSRC)/pipe_wide.hip $(CSRC)/pipe_wide_paths.hip $(CSRC)/pipe_paths.hip \
+             $(CSRC)/spec2.hip
 HOST_SRCS := $(CSRC)/runtime.cpp $(CSRC)/svh_api.cpp $(CSRC)/HIP_impl.cpp $(CSRC)/data_reader.cpp $(CSRC)/stream.cpp \
              $(CSRC)/seqreader.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS))

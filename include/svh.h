@@ -86,8 +86,13 @@ typedef struct {
     int32_t kernel;      /* SVH_KERNEL_* */
     int32_t max_threads; /* workgroup size cap (multiple of 64, <= 1024; the fused kernel caps at
                             512); 0 = each kernel's default */
-    int32_t reserved;
+    int32_t flags;       /* SVH_MODEL_* bits (0: defaults) */
 } svh_model_opts;
+
+/* svh_model_opts.flags: _spec level 2 streams the dense products (the path used for level >= 3)
+ * instead of evaluating each chunk from the folded sparse matrices on chip (A/B and tests; the
+ * results are identical) */
+#define SVH_MODEL_SPEC_DENSE 1
 
 /* emissions: S x n, symbol-major (HMM::emissions[symbol][state]); transitions as COO
  * src -> dst (HMM::trans_rows / trans_cols / trans_probs); duplicates: first one wins
@@ -178,6 +183,11 @@ int svh_batch_plan(svh_batch_t b, uint32_t level, svh_model_info* info);
  * were re-run by the serial chain kernel (results are identical either way); 0 if the last run
  * did not use the pipelined kernel.  Waits for the run. */
 int svh_batch_fallbacks(svh_batch_t b, uint64_t* rows);
+/* Whether this build holds the pipelined latency kernel at `slots` x `waves` with step table mode
+ * `table_mode` (pipe_kernel.h TM; SVH_PIPE_SM / SVH_PIPE_WAVES / SVH_PIPE_TM select them).  The
+ * default build holds the geometry and modes AUTO plans (2 x 4; TM 4, and TM 0 for alphabets of
+ * more than 20 symbols); the others are A/B builds' (-DSVH_PIPE_AB_ALL).  *built = 1 or 0. */
+int svh_pipe_variant_built(int32_t slots, int32_t waves, int32_t table_mode, int32_t* built);
 int svh_batch_destroy(svh_batch_t b);
 /* Diagnostics: mark the batch's last run (enqueued on `stream`) as if one of its bounded waits
  * had given up, so its next svh_batch_read fails with SVH_E_HIP.  Every batch has a fault word of

@@ -33,6 +33,7 @@ SVH_KERNEL_CHAIN = 4
 SVH_KERNEL_PIPE = 5
 SVH_KERNEL_PIPE_WIDE = 6
 SVH_BATCH_PATHS = 1
+SVH_MODEL_SPEC_DENSE = 1
 
 
 class SvhError(RuntimeError):
@@ -44,7 +45,7 @@ class SvhError(RuntimeError):
 
 
 class svh_model_opts(ctypes.Structure):
-    _fields_ = [("device", c_int32), ("kernel", c_int32), ("max_threads", c_int32), ("reserved", c_int32)]
+    _fields_ = [("device", c_int32), ("kernel", c_int32), ("max_threads", c_int32), ("flags", c_int32)]
 
 
 class svh_model_info(ctypes.Structure):
@@ -91,6 +92,7 @@ SIGNATURES = {
     "svh_batch_elapsed_ms": (c_int, [c_void_p, P_f32]),
     "svh_batch_plan": (c_int, [c_void_p, c_uint32, POINTER(svh_model_info)]),
     "svh_batch_fallbacks": (c_int, [c_void_p, P_u64]),
+    "svh_pipe_variant_built": (c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, POINTER(ctypes.c_int32)]),
     "svh_batch_debug_fault": (c_int, [c_void_p, c_void_p]),
     "svh_batch_destroy": (c_int, [c_void_p]),
     "svh_viterbi": (c_int, [c_void_p, c_uint32, c_uint64, P_u64, P_u64, P_f32, P_i64, P_i32]),
@@ -146,3 +148,10 @@ def device_count() -> int:
     c = c_int32(0)
     check(lib.svh_device_count(ctypes.byref(c)))
     return int(c.value)
+
+
+def pipe_variant_built(slots: int, waves: int, table_mode: int) -> bool:
+    """svh_pipe_variant_built: is this latency-kernel variant in the loaded build?"""
+    r = ctypes.c_int32()
+    check(lib.svh_pipe_variant_built(slots, waves, table_mode, ctypes.byref(r)))
+    return bool(r.value)

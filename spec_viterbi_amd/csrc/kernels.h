@@ -223,24 +223,28 @@ struct PipeModel {
 };
 constexpr int kPipeStamps = 13;  // written only by -DSVH_PIPE_DIAG builds of pipe.hip
 // Per-batch scratch of the pipelined kernel (sized for `rows` rows).
+constexpr uint32_t kCtrClass = 4, kCtrLeft = 12, kCtrWords = 16;
 struct PipeScratch {
-    uint32_t* ctr;    // [4]: [0] workgroup ticket, [1] finished workgroups, [2] last epoch
+    uint32_t* ctr;    // [kCtrWords]: [0] workgroup ticket, [1] finished workgroups, [2] last epoch,
+                      // [kCtrClass + r] per-class tickets (r < 8), [kCtrLeft] leftover tickets (x.xmap)
     uint32_t* done;   // [rows] finished workgroups of row q (reset by its last one)
     uint64_t* part;   // [rows][G][2]: {C min | violation, (best value, best row) key}
     uint64_t* gran;   // [rows][G-1][kPipeGRing] tagged boundary granules {score, tag}
     uint32_t* cons;   // [rows][G] granules received by workgroup g's first wave
     uint32_t* viol;   // [rows] 1: speculation failed, row needs the serial kernel
     uint32_t* xcc;    // [rows][G] (epoch << 4) | XCC id of workgroup g of row q (XCD-local hand-offs)
-    uint32_t xmap;    // launch: 1 = (row, workgroup) from blockIdx by XCD class (every workgroup resident)
+    uint32_t xmap;    // launch: 1 = (row, workgroup) from per-XCD-class tickets (pipe_kernel.h)
     uint32_t rows, G;
 };
 constexpr uint32_t kPairSymbols = 20;  // pipe_kernel.h kPairSym: the pair tables' symbol capacity
 __host__ __device__ inline size_t pipe_lds_bytes(uint32_t W, uint32_t S) {
     // boundary ring [W][kPipeRing][64] | counters [16] | heavy constants [S][8] | reduction [W][4] | ticket
-    // | [3] pad | counter-publish sink [W][64] (lanes 1..63 of a count store write there)
-    return ((size_t)W * kPipeRing * 64 + 16 + (size_t)S * 8 + (size_t)W * 4 + 4 + (size_t)W * 64) * 4;
+    return ((size_t)W * kPipeRing * 64 + 16 + (size_t)S * 8 + (size_t)W * 4 + 4) * 4;
 }
 bool pipe_supported(int sm, int waves, bool sx);
+// table mode tm (pipe_kernel.h TM) compiled into this build at the default geometry (TM 1..3 and
+// the other geometries only in SVH_PIPE_AB_ALL builds)
+bool pipe_tm_supported(int tm);
 // b.cmask != nullptr selects the decoded-path variant (every sequence must start at step 0).
 hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
 bool pipe_paths_supported(int sm, int waves);
@@ -379,6 +383,73 @@ struct SpecChunkBatch {
 };
 hipError_t launch_spec_chunk(const CsrModel& m, const float* products, const SpecChunkBatch& c,
                              uint32_t pstride, hipStream_t stream);
+// _spec level 2 on chip (spec2.hip): one persistent workgroup of kSpec2Threads per sequence runs
+// every chunk of two observations from the folded sparse matrices (no dense products).
+// Rows with at most kSpec2LightMax terms are light (their terms in registers of the thread
+// r % 1024, slot r / 1024), the others heavy (their terms spread over the threads, x = hs * 1024 +
+// t, sorted by row).  Columns are packed as m | (heavy index of m + 1) << 16 (0: m is light).
+constexpr uint32_t kSpec2Threads = 1024;
+constexpr uint32_t kSpec2LightMax = 4;
+struct Spec2Model {
+    const float* emis;     // [S][n]
+    const uint32_t* lcol;  // [R][KL][1024] packed columns of the light rows' terms (0xFFFFFFFF: none)
+    const float* lval;     // [R][KL][1024] T^T values
+    const uint32_t* hcol;  // [NHS * 1024] packed columns of the heavy terms
+    const float* hval;     // [NHS * 1024]
+    const uint32_t* hhid;  // [NHS * 1024] heavy index of the term's row (0xFFFFFFFF: padding)
+    const uint32_t* hrow;  // [H] state of heavy row h
+    const uint32_t* hoff;  // [H + 1] first term of heavy row h
+    const float* amax;     // [H] max over symbols and out-terms (j, p) of the finite fl(E_s[j] + T^T[j][p])
+    uint32_t n, S, H, NH;
+    uint32_t R, KL, NHS;   // instantiated sizes (rounded: 2/4, 2/4, 4/8)
+    uint32_t prune;        // every score >= 0: candidates pruned (spec2.hip); 0: every term kept
+};
+struct Spec2Batch {
+    const uint8_t* symbols;
+    const uint64_t* sym_off;
+    const uint32_t* len;      // [nseq] sequence lengths
+    const uint32_t* nchunks;  // [nseq] floor((len - 1) / 2)
+    float* v;                 // [nseq][n] in: the state after observation 0; out: after the chunks
+    uint32_t nseq;
+};
+struct Spec2Lds {
+    uint32_t v, lp, hp, cl, hacc, cmin, ccnt, eh, hoff, amax;  // offsets in floats (16-byte aligned)
+    size_t bytes;
+};
+__host__ __device__ inline uint32_t spec2_al4(uint32_t x) { return (x + 3u) & ~3u; }
+__host__ __device__ inline Spec2Lds spec2_lds_layout(uint32_t n, uint32_t KL, uint32_t NH, uint32_t H) {
+    // v [n] | LP [n][KL] float2 | HP [NH] float2 | CL [NH] u16 | hacc [H] | cmin [2][H] | ccnt [2][H]
+    // | EH [2][2][H] | hoff [H + 1] | amax [H]
+    Spec2Lds L;
+    uint32_t o = 0;
+    L.v = o;
+    o += spec2_al4(n);
+    L.lp = o;
+    o += spec2_al4(2 * n * KL);
+    L.hp = o;
+    o += spec2_al4(2 * NH);
+    L.cl = o;
+    o += spec2_al4((NH + 1) / 2);
+    L.hacc = o;
+    o += spec2_al4(H);
+    L.cmin = o;
+    o += spec2_al4(2 * H);
+    L.ccnt = o;
+    o += spec2_al4(2 * H);
+    L.eh = o;
+    o += spec2_al4(4 * H);
+    L.hoff = o;
+    o += spec2_al4(H + 1);
+    L.amax = o;
+    o += spec2_al4(H);
+    L.bytes = (size_t)o * 4;
+    return L;
+}
+uint32_t spec2_round_r(uint32_t R);
+uint32_t spec2_round_kl(uint32_t KL);
+uint32_t spec2_round_nhs(uint32_t NHS);
+hipError_t launch_spec2(const Spec2Model& m, const Spec2Batch& b, hipStream_t stream);
+
 // Time-parallel helpers (timepar.hip; Batch::run_time_parallel).  Row index tables per active
 // segment r: probe run from the exact start (x; the probe from the start's light part is row
 // x + xl_off), first of the segment's guess probe rows (g: the light guess, then one row per basis

@@ -28,16 +28,22 @@ const void* pipe_kernel_tm0(int sm, int waves, bool sx, int paths) {
         return paths == 2 ? pipe_ptr<2, 4, 2>(sx) : pipe_ptr<2, 4, 1>(sx);
     }
     switch (sm * 100 + waves) {
+        case 204: return pipe_ptr<2, 4>(sx);  // the geometry AUTO plans (alphabets of 21..32 symbols)
+#ifdef SVH_PIPE_AB_ALL  // A/B and geometry-test builds: the geometries measured against it
         case 104: return pipe_ptr<1, 4>(sx);
         case 108: return pipe_ptr<1, 8>(sx);
-        case 204: return pipe_ptr<2, 4>(sx);
         case 208: return pipe_ptr<2, 8>(sx);
+#endif
         default: return nullptr;
     }
 #endif
 }
 
 bool pipe_supported(int sm, int waves, bool sx) { return pipe_kernel_tm0(sm, waves, sx, 0) != nullptr; }
+bool pipe_tm_supported(int tm) {
+    if (tm == 0) return true;
+    return tm >= 1 && tm <= 4 && pipe_kernel_tm1(2, 4, false, tm >= 2 ? -tm : 0) != nullptr;
+}
 bool pipe_paths_supported(int sm, int waves) { return pipe_kernel_tm0(sm, waves, false, 1) != nullptr; }
 
 hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream) {
@@ -58,17 +64,14 @@ hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratc
     PipeScratch xx = x;
     void* args[] = {&mm, &bb, &xx};
     const uint64_t grid = (uint64_t)b.nseq * m.G;
-    // XCD-class mapping of rows to workgroups while the launch is resident at one workgroup per
-    // CU (pipe_kernel.h); SVH_PIPE_XMAP=0 keeps the dynamic tickets (A/B)
+    // XCD-class mapping of rows to workgroups when the launch fits the chip at one workgroup per CU
+    // (pipe_kernel.h: per-class tickets in start order, deadlock-free whatever else holds CUs; the
+    // size condition is about speed only); SVH_PIPE_XMAP=0 keeps the single ticket counter (A/B)
     static const bool xmap_env = !(std::getenv("SVH_PIPE_XMAP") && std::atoi(std::getenv("SVH_PIPE_XMAP")) == 0);
     xx.xmap = xmap_env && m.cus && grid <= m.cus ? 1u : 0u;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const size_t lds = paths ? (pipe_lds_bytes(m.W, m.S) + 15) / 16 * 16 + pipe_path_lds_bytes(m.W)
-                             : pipe_lds_bytes(m.W, m.S)
-#ifdef SVH_PIPE_G16  // A/B experiment: the 64-slot ring of pipe_kernel_g16.h
-                                   + (size_t)m.W * 32 * 64 * 4
-#endif
-        ;
+                             : pipe_lds_bytes(m.W, m.S);
     if (lds > 64 * 1024) {  // more than 64 KiB of dynamic LDS: a host-side attribute of the function
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

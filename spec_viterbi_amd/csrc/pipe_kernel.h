@@ -105,26 +105,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 #define SVH_PIPE_XL 1
 #endif
 
-// The granule consumer's progress store (once per 32 observations, after the prefetch of the last
-// group) is a vector-memory operation too: the next iteration's first two groups have it queued
-// after their own prefetch, so they wait for one operation more than kGpf - 1, or the in-order
-// vmcnt would make them wait for the younger prefetch (issued one group earlier) as well.  A/B knob
-// (SVH_PIPE_VMS=0: the old count).
-#ifndef SVH_PIPE_VMS
-#define SVH_PIPE_VMS 0
-#endif
-
-// Publishing a wave's count (A/B knob SVH_PIPE_PUT): 0 = one lane's store with EXEC narrowed to
-// lane 0 inside the asm (lds_put1); 1 = every lane stores, lane 0 to the count and lanes 1..63 to
-// a sink of their own (a per-lane address vector built once: no EXEC writes, no s_nop).
-#ifndef SVH_PIPE_PUT
-#define SVH_PIPE_PUT 0
-#endif
-__device__ __forceinline__ void lds_put_v(uint32_t vaddr, uint32_t v) {
-    asm volatile("ds_write_b32 %0, %1" ::"v"(vaddr), "v"(v) : "memory");
-}
-// One lane's LDS store of a wave-uniform word: EXEC narrowed to lane 0 inside the asm (no
-// divergent branch in the compiler's view).
+// One lane's LDS store of a wave-uniform word (a wave's count): EXEC narrowed to lane 0 inside the
+// asm (no divergent branch in the compiler's view).  Measured and not kept (round 4): every lane
+// storing, lanes 1..63 into a sink of their own (no EXEC writes), within noise.
 __device__ __forceinline__ void lds_put1(uint32_t addr, uint32_t v) {
     uint64_t saved;
     asm volatile(
@@ -271,37 +254,44 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t w = (uint32_t)uniform((int)(tid >> 6));
     const uint32_t S = m.S, P = m.P, G = m.G;
-    if (tid == 0) *tick = __hip_atomic_fetch_add(x.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (row, workgroup) of this workgroup, from a ticket taken in start order, so a consumer's
+    // producer has always started before it (no deadlock when the grid exceeds residency or other
+    // launches hold CUs).  Default: one ticket counter, rows in ticket order.  x.xmap (the runtime
+    // sets it when the launch fits the chip at one workgroup per CU): per-class tickets, so that a
+    // row's G workgroups share an XCD class (blocks b and b + 8 share an XCD under the observed
+    // round-robin placement; speed only -- the hand-offs check the real XCC ids, SVH_PIPE_XL).
+    // Class r = b % 8 holds n_r blocks and takes f_r = n_r / G rows whole: its k-th ticket (k <
+    // f_r G) is member k % G of its (k / G)-th row.  Its remaining tickets take a second ticket from
+    // one shared leftover counter, which forms the remaining rows in that counter's order.  Within a
+    // class and within the leftover rows the members of a row are numbered in start order, as
+    // with the single counter.
+    if (tid == 0) {
+        uint32_t t;
+        if (x.xmap) {
+            const uint32_t N = gridDim.x, r = blockIdx.x & 7u;
+            uint32_t pf = 0, fr = 0, F = 0;
+            for (uint32_t rr = 0; rr < 8; ++rr) {
+                const uint32_t n = N > rr ? (N - rr + 7) / 8 : 0, f = n / G;
+                F += f;
+                if (rr < r) pf += f;
+                if (rr == r) fr = f;
+            }
+            const uint32_t k = __hip_atomic_fetch_add(x.ctr + kCtrClass + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k < fr * G) {
+                t = (pf + k / G) * G + k % G;
+            } else {
+                const uint32_t u = __hip_atomic_fetch_add(x.ctr + kCtrLeft, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                t = (F + u / G) * G + u % G;
+            }
+        } else {
+            t = __hip_atomic_fetch_add(x.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *tick = t;
+    }
     if (tid < 16) cnt[tid] = 0;
     for (uint32_t i = tid; i < S * 8; i += 64 * W) ctab[i] = m.hc[i];
     __syncthreads();
-    // (row, workgroup) of this workgroup.  Dynamic tickets in start order by default (a consumer's
-    // producer has always started: no deadlock when the grid exceeds residency).  x.xmap (the
-    // runtime sets it only when every workgroup of the launch is resident): by blockIdx, so that
-    // a row's G workgroups share an XCD class (blocks b and b + 8 share an XCD under the observed
-    // round-robin placement; speed only -- the hand-offs check the real XCC ids, SVH_PIPE_XL):
-    // class r = b % 8 takes rows whole, G consecutive members each, and the classes' leftover
-    // members form the remaining rows in class order.
-    uint32_t id = (uint32_t)uniform((int)*tick);
-    if (x.xmap) {
-        const uint32_t N = gridDim.x, r = blockIdx.x & 7u, k = blockIdx.x >> 3;
-        uint32_t pf = 0, po = 0, fr = 0, F = 0;
-        for (uint32_t rr = 0; rr < 8; ++rr) {
-            const uint32_t n = N > rr ? (N - rr + 7) / 8 : 0, f = n / G;
-            F += f;
-            if (rr < r) {
-                pf += f;
-                po += n - f * G;
-            }
-            if (rr == r) fr = f;
-        }
-        if (k < fr * G) {
-            id = (pf + k / G) * G + k % G;
-        } else {
-            const uint32_t u = po + (k - fr * G);
-            id = (F + u / G) * G + u % G;
-        }
-    }
+    const uint32_t id = (uint32_t)uniform((int)*tick);
     const uint32_t q = id / G, g = id - q * G;
     const uint32_t ep = (uint32_t)uniform((int)__hip_atomic_load(x.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
 #if SVH_PIPE_XL
@@ -730,12 +720,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         const float* const ring_prev = ring_w - kR * 64;
         uint32_t* const cnt_w = cnt + w;
         const uint32_t cnt_addr = lds_addr(cnt_w);
-        // SVH_PIPE_PUT 1: lane 0 -> the count, lane l > 0 -> sink[w][l]
-        const uint32_t cnt_vaddr = lane == 0 ? cnt_addr : lds_addr(tick + 4 + (w * 64 + lane));
-        auto put_cnt = [&](uint32_t val) {
-            if constexpr (SVH_PIPE_PUT) lds_put_v(cnt_vaddr, val);
-            else lds_put1(cnt_addr, val);
-        };
+        auto put_cnt = [&](uint32_t val) { lds_put1(cnt_addr, val); };
         uint64_t* const gin = x.gran + ((size_t)q * (G - 1) + (g - 1)) * kGR;  // src == 2
         uint64_t* const gout = x.gran + ((size_t)q * (G - 1) + g) * kGR;       // dst == 2
         uint64_t* const cons_in = reinterpret_cast<uint64_t*>(x.cons) + (size_t)q * G + g;      // src == 2 publishes
@@ -760,12 +745,14 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         };
         bool gran_plain = false, cons_plain = false;
         // granule / progress-word stores: plain when the reader shares this XCD (SVH_PIPE_XL)
+        // (a plain store is a relaxed atomic store at wavefront scope: the same unflagged
+        // global_store as `*a = v64`, but one the compiler may not tear, merge or sink)
         auto st_gran = [&](uint64_t* a, uint64_t v64) {
-            if (SVH_PIPE_XL && gran_plain) *a = v64;
+            if (SVH_PIPE_XL && gran_plain) __hip_atomic_store(a, v64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             else g_st64(a, v64);
         };
         auto st_cons = [&](uint64_t v64) {
-            if (SVH_PIPE_XL && cons_plain) *cons_in = v64;
+            if (SVH_PIPE_XL && cons_plain) __hip_atomic_store(cons_in, v64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             else g_st64(cons_in, v64);
         };
         // wait until the previous wave has published observations < need
@@ -893,16 +880,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             // body: 32 observations per iteration, four groups of 8
             if (t + 32 <= len) {
                 uint64_t gq[kGpf] = {};  // SRC 2: granule groups in flight
-                // SRC 2 waves whose only body stores are the progress words (see SVH_PIPE_VMS)
-                constexpr bool kVmStore = SVH_PIPE_VMS && SRC == 2 && DST != 2 && PATHS == 0 && kGpf == 2;
                 if constexpr (SRC == 2) {
 #pragma unroll
                     for (uint32_t j = 0; j < kGpf; ++j) g_prefetch64(gq[j], gin + ((t + 8 * j + (lane & 7u)) & (kGR - 1)));
-                    // store-aware counts: the first iteration's first two groups also find one store
-                    // queued behind their prefetches (the progress word again: observations < t done)
-                    if constexpr (kVmStore) {
-                        if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | t);
-                    }
                 }
                 float gpend = 0.0f;    // DST 2: the previous group's boundary scores (lanes 0..7),
                 uint32_t gpend_t = 0;  // read back from the ring one group before they are stored
@@ -947,9 +927,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         float bv = kInf;  // lanes 0..7: the previous block's last scores of tg..tg+7
                         float gl[8];      // SVH_PIPE_RING8: this group's last-slot scores
                         if constexpr (SRC == 2) {
-                            // gq[j]: kGpf - 1 later loads in flight (+ the progress store, groups 0, 1)
-                            if constexpr (kVmStore && j < 2) wait_vmcnt<kGpf>();
-                            else wait_vmcnt<kGpf - 1>();
+                            wait_vmcnt<kGpf - 1>();  // gq[j]: kGpf - 1 later loads in flight
                             uint64_t gv = gq[j % kGpf];
                             while (__builtin_amdgcn_ballot_w64((uint32_t)(gv >> 32) != gtag(ep, tg)) != 0) {
                                 if (dbg) ++dg[5];
@@ -1179,6 +1157,8 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             __hip_atomic_store(x.ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(x.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(x.ctr + 2, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (uint32_t c = kCtrClass; c <= kCtrLeft; ++c)
+                __hip_atomic_store(x.ctr + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

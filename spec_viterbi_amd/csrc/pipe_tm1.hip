@@ -1,6 +1,6 @@
-// Pipelined chain Viterbi kernel, TM = 1 (pair tables read by 64-bit moves; pipe_kernel.h):
-// scores-only instantiations, 2 slots per lane, 4 waves per workgroup (one per SIMD: the 258
-// registers of the pair tables do not fit the 256 of two waves per SIMD, which spilled).
+// Pipelined chain Viterbi kernel, pair tables (pipe_kernel.h TM = 4, the default; TM = 1..3 in
+// SVH_PIPE_AB_ALL builds only): scores-only instantiations, 2 slots per lane, 4 waves per workgroup
+// (one per SIMD: the 258 registers of the pair tables do not fit the 256 of two waves per SIMD).
 // The LDS boundary ring of these instantiations is batched per group of 8 (SVH_PIPE_RING8 = 1: two
 // ds_write_b128 per group instead of a ds_write_b32 per step).  With the pair-table step the
 // per-step LDS store paced the pipeline: 0.363 -> 0.282 ms on the headline (profiles/r04_s4/ab.log;
@@ -8,11 +8,7 @@
 #ifndef SVH_PIPE_RING8
 #define SVH_PIPE_RING8 1
 #endif
-#ifdef SVH_PIPE_G16  // A/B experiment: groups of 16 observations (pipe_kernel_g16.h)
-#include "pipe_kernel_g16.h"
-#else
 #include "pipe_kernel.h"
-#endif
 
 namespace svh {
 
@@ -25,17 +21,21 @@ const void* pipe_kernel_tm1(int sm, int waves, bool sx, int paths) {
     return waves == 4 && !sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 1>) : nullptr;
 #else
     if (waves != 4) return nullptr;
-    if (paths == -2)  // TM = 2 (indexed operands; A/B: SVH_PIPE_TM=2)
-        return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 2>)
-                  : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 2>);
-    if (paths == -3)  // TM = 3 (packed feeder terms; A/B: SVH_PIPE_TM=3)
-        return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 3>)
-                  : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 3>);
-    if (paths == -4)  // TM = 4 (indexed operands, packed feeder terms; A/B: SVH_PIPE_TM=4)
+    if (paths == -4)  // TM = 4 (indexed operands, packed feeder terms): the mode AUTO selects
         return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 4>)
                   : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 4>);
-    return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 1>)
-              : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 1>);
+#ifdef SVH_PIPE_AB_ALL  // A/B and table-mode-test builds: the modes measured against it
+    if (paths == -2)  // TM = 2 (indexed operands; SVH_PIPE_TM=2)
+        return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 2>)
+                  : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 2>);
+    if (paths == -3)  // TM = 3 (packed feeder terms; SVH_PIPE_TM=3)
+        return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 3>)
+                  : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 3>);
+    if (paths == 0)  // TM = 1 (pair tables by 64-bit moves; SVH_PIPE_TM=1)
+        return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 1>)
+                  : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 1>);
+#endif
+    return nullptr;
 #endif
 }
 

@@ -787,7 +787,7 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     view.tm = !p.wide && p.SM == 2 && p.W == 4 && S <= kPairSymbols ? 4u : 0u;
     if (const char* e = std::getenv("SVH_PIPE_TM"); e) {
         const int t = std::atoi(e);
-        if (t == 0 || (t >= 1 && t <= 4 && view.tm)) view.tm = (uint32_t)t;
+        if (t == 0 || (t >= 1 && t <= 4 && view.tm && pipe_tm_supported(t))) view.tm = (uint32_t)t;
     }
     if (const char* e = std::getenv("SVH_PIPE_DEBUG"); e && std::atoi(e)) {  // diagnostics only
         d_stamps.alloc((size_t)65536 * kPipeStamps * 8);
@@ -861,8 +861,8 @@ void DevicePipePlan::report_stamps(uint32_t nseq) const {
 
 void PipeScratchBuffers::ensure(uint32_t rows, uint32_t G, hipStream_t s) {
     if (!d_ctr.ptr) {
-        d_ctr.alloc(16);
-        hip_check(hipMemsetAsync(d_ctr.ptr, 0, 16, s), "pipe counters");
+        d_ctr.alloc(kCtrWords * 4);
+        hip_check(hipMemsetAsync(d_ctr.ptr, 0, kCtrWords * 4, s), "pipe counters");
     }
     if (view.ctr && rows <= view.rows && G <= view.G) return;
     rows = std::max(rows, view.rows);
@@ -953,6 +953,7 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
     if (dev < 0) hip_check(hipGetDevice(&dev), "hipGetDevice");
     device = dev;
     kernel_pref = opts ? opts->kernel : SVH_KERNEL_AUTO;
+    spec_dense = opts && (opts->flags & SVH_MODEL_SPEC_DENSE);
     // 0 = each planner's default; the fused kernel caps at kMaxFusedThreads, the chain kernel at
     // kMaxBandThreads.
     const int max_threads = (opts && opts->max_threads > 0) ? opts->max_threads : 0;
@@ -1110,15 +1111,140 @@ const DevicePlan* Model::plan_for(bool paths) const {
     return (p && p->plan.fused) ? p : nullptr;
 }
 
+// ------------------------------------------------------------------------------------------
+// _spec level 2 on chip (spec2.hip).  Light rows (<= kSpec2LightMax terms) keep their terms in the
+// registers of thread r % 1024, slot r / 1024; heavy rows' terms are spread over the threads in row
+// order.  amax[h] bounds every finite a = fl(E_s[j] + T^T[j][p]) that meets heavy row p = hrow[h]
+// in a chunk (the candidate pruning's bound); prune only when every score is >= 0.
+// ------------------------------------------------------------------------------------------
+Spec2Plan make_spec2_plan(const HostModel& hm) {
+    Spec2Plan sp;
+    const uint32_t n = hm.n, S = hm.S, T = kSpec2Threads;
+    if (n == 0 || n > 65535 || n > 4 * T) return sp;
+    std::vector<int32_t> hid(n, -1);
+    uint32_t klmax = 1, NH = 0;
+    for (uint32_t r = 0; r < n; ++r) {
+        const uint32_t deg = hm.rowptr[r + 1] - hm.rowptr[r];
+        if (deg > kSpec2LightMax) {
+            hid[r] = (int32_t)sp.hrow.size();
+            sp.hrow.push_back(r);
+            NH += deg;
+        } else {
+            klmax = std::max(klmax, deg);
+        }
+    }
+    const uint32_t H = (uint32_t)sp.hrow.size();
+    sp.R = spec2_round_r((n + T - 1) / T);
+    sp.KL = spec2_round_kl(klmax);
+    sp.NHS = spec2_round_nhs(std::max<uint32_t>((NH + T - 1) / T, 1));
+    if (!sp.R || !sp.KL || !sp.NHS || H > T || NH > 65535) return sp;
+    if (spec2_lds_layout(n, sp.KL, NH, H).bytes > kMaxLdsBytes) return sp;
+    auto packed = [&](uint32_t m) { return m | ((uint32_t)(hid[m] + 1) << 16); };
+    sp.H = H;
+    sp.NH = NH;
+    sp.lcol.assign((size_t)sp.R * sp.KL * T, 0xFFFFFFFFu);
+    sp.lval.assign((size_t)sp.R * sp.KL * T, kInfH);
+    for (uint32_t r = 0; r < n; ++r) {
+        if (hid[r] >= 0) continue;
+        const uint32_t s = r / T, t = r % T;
+        for (uint32_t e = hm.rowptr[r], k = 0; e < hm.rowptr[r + 1]; ++e, ++k) {
+            sp.lcol[((size_t)s * sp.KL + k) * T + t] = packed(hm.col[e]);
+            sp.lval[((size_t)s * sp.KL + k) * T + t] = hm.val[e];
+        }
+    }
+    sp.hcol.assign((size_t)sp.NHS * T, 0xFFFFFFFFu);
+    sp.hval.assign((size_t)sp.NHS * T, kInfH);
+    sp.hhid.assign((size_t)sp.NHS * T, 0xFFFFFFFFu);
+    sp.hoff.assign(H + 1, 0);
+    uint32_t x = 0;
+    for (uint32_t h = 0; h < H; ++h) {
+        const uint32_t r = sp.hrow[h];
+        sp.hoff[h] = x;
+        for (uint32_t e = hm.rowptr[r]; e < hm.rowptr[r + 1]; ++e, ++x) {
+            sp.hcol[x] = packed(hm.col[e]);
+            sp.hval[x] = hm.val[e];
+            sp.hhid[x] = h;
+        }
+    }
+    sp.hoff[H] = x;
+    // a of the terms (j, p) with p heavy, over every symbol: fl(E_s[j] + T^T[j][p]) (float adds)
+    sp.amax.assign(H, 0.0f);
+    bool nonneg = true;
+    for (uint32_t j = 0; j < n; ++j)
+        for (uint32_t e = hm.rowptr[j]; e < hm.rowptr[j + 1]; ++e) {
+            nonneg = nonneg && hm.val[e] >= 0.0f;
+            const int32_t h = hid[hm.col[e]];
+            if (h < 0) continue;
+            for (uint32_t o = 0; o < S; ++o) {
+                const float a = hm.emis[(size_t)o * n + j] + hm.val[e];
+                if (a < kInfH) sp.amax[h] = std::max(sp.amax[h], a);
+            }
+        }
+    for (float e : hm.emis) nonneg = nonneg && e >= 0.0f;
+    for (float e : hm.start) nonneg = nonneg && e >= 0.0f;
+    sp.prune = nonneg;
+    sp.ok = true;
+    return sp;
+}
+
+void DeviceSpec2Plan::upload(const Spec2Plan& p, const HostModel& hm, const float* d_emis, hipStream_t s) {
+    plan = p;
+    std::memset(&view, 0, sizeof(view));
+    if (!p.ok) return;
+    d_lcol.upload(p.lcol.data(), p.lcol.size() * 4, s);
+    d_lval.upload(p.lval.data(), p.lval.size() * 4, s);
+    d_hcol.upload(p.hcol.data(), p.hcol.size() * 4, s);
+    d_hval.upload(p.hval.data(), p.hval.size() * 4, s);
+    d_hhid.upload(p.hhid.data(), p.hhid.size() * 4, s);
+    d_hrow.upload(p.hrow.data(), std::max<size_t>(p.hrow.size(), 1) * 4, s);
+    d_hoff.upload(p.hoff.data(), p.hoff.size() * 4, s);
+    d_amax.upload(p.amax.data(), std::max<size_t>(p.amax.size(), 1) * 4, s);
+    view.emis = d_emis;
+    view.lcol = d_lcol.as<uint32_t>();
+    view.lval = d_lval.as<float>();
+    view.hcol = d_hcol.as<uint32_t>();
+    view.hval = d_hval.as<float>();
+    view.hhid = d_hhid.as<uint32_t>();
+    view.hrow = d_hrow.as<uint32_t>();
+    view.hoff = d_hoff.as<uint32_t>();
+    view.amax = d_amax.as<float>();
+    view.n = hm.n;
+    view.S = hm.S;
+    view.H = p.H;
+    view.NH = p.NH;
+    view.R = p.R;
+    view.KL = p.KL;
+    view.NHS = p.NHS;
+    view.prune = p.prune ? 1u : 0u;
+}
+
 void Model::spec_build(uint32_t level, hipStream_t s) {
     std::lock_guard<std::mutex> lock(mu);
     DeviceGuard g(device);
     if (!s) s = stream;
     d_products = DeviceBuffer();
     spec_level = 0;
+    spec2_on = false;
     if (level <= 1) {
         spec_level = level;
         return;
+    }
+    // level 2: the on-chip kernel when the model fits it (no products: the chunks are evaluated
+    // from the folded sparse matrices, spec2.hip); SVH_SPEC_DENSE=1 streams the dense products (A/B)
+    static const bool dense_env = std::getenv("SVH_SPEC_DENSE") && std::atoi(std::getenv("SVH_SPEC_DENSE")) == 1;
+    if (level == 2 && !dense_env && !spec_dense) {
+        if (!spec2.plan.ok) {
+            const Spec2Plan sp = make_spec2_plan(host);
+            if (sp.ok) {
+                spec2.upload(sp, host, d_gemis.as<float>(), s);
+                hip_check(hipStreamSynchronize(s), "spec2 plan upload");
+            }
+        }
+        if (spec2.plan.ok) {
+            spec2_on = true;
+            spec_level = level;
+            return;
+        }
     }
     const CsrModel c = csr_view();
     if (host.n > 65535) throw Error(SVH_E_UNSUPPORTED, "_spec level >= 2 needs states_num <= 65535");
@@ -1533,12 +1659,14 @@ void Batch::run(uint32_t level, hipStream_t s) {
                       "traceback kernel");
     } else {
         const uint32_t n = model->host.n;
-        if (spec_ready_level != level) {
+        const bool on_chip = level == 2 && model->spec2_on;
+        const uint32_t ready = level | (on_chip ? 0x100u : 0u);
+        if (spec_ready_level != ready) {
             std::vector<uint32_t> nch(nseq), tb(nseq), vrow(nseq);
             for (uint32_t q = 0; q < nseq; ++q) {
                 nch[q] = (lens[q] - 1) / level;
                 tb[q] = 1 + nch[q] * level;
-                vrow[q] = (nch[q] & 1u) * nseq + q;
+                vrow[q] = on_chip ? q : (nch[q] & 1u) * nseq + q;  // the row the chunks end in
             }
             d_nchunks.upload(nch.data(), nch.size() * 4, s);
             d_tbegin.upload(tb.data(), tb.size() * 4, s);
@@ -1547,17 +1675,27 @@ void Batch::run(uint32_t level, hipStream_t s) {
             hip_check(hipStreamSynchronize(s), "spec batch setup");
             max_chunks = 0;
             for (uint32_t q = 0; q < nseq; ++q) max_chunks = std::max(max_chunks, nch[q]);
-            spec_ready_level = level;
+            spec_ready_level = ready;
         }
         float* vb = d_vbuf.as<float>();
         hip_check(launch_first_step(csr, fb.symbols, fb.sym_off, nseq, vb, s), "spec first step");
+        if (on_chip) {  // every chunk of every sequence in one launch, v in place (row q)
+            Spec2Batch sb;
+            sb.symbols = fb.symbols;
+            sb.sym_off = fb.sym_off;
+            sb.len = p_end;
+            sb.nchunks = d_nchunks.as<uint32_t>();
+            sb.v = vb;
+            sb.nseq = nseq;
+            hip_check(launch_spec2(model->spec2.view, sb, s), "spec2 kernel");
+        }
         SpecChunkBatch cb;
         cb.symbols = fb.symbols;
         cb.sym_off = fb.sym_off;
         cb.nchunks = d_nchunks.as<uint32_t>();
         cb.nseq = nseq;
         cb.level = level;
-        for (uint32_t c = 0; c < max_chunks; ++c) {
+        for (uint32_t c = 0; c < (on_chip ? 0u : max_chunks); ++c) {
             cb.chunk = c;
             cb.v_src = vb + (size_t)(c & 1u) * nseq * n;
             cb.v_dst = vb + (size_t)((c + 1) & 1u) * nseq * n;

@@ -156,6 +156,24 @@ struct DevicePipePlan {
     void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_PIPE_DEBUG): first sequence's waves
 };
 
+// Host tables of the on-chip _spec level-2 kernel (spec2.hip); ok == false when the model does
+// not fit it (then level 2 streams dense products).
+struct Spec2Plan {
+    bool ok = false;
+    bool prune = false;
+    uint32_t R = 0, KL = 0, NHS = 0, H = 0, NH = 0;
+    std::vector<uint32_t> lcol, hcol, hhid, hrow, hoff;
+    std::vector<float> lval, hval, amax;
+};
+Spec2Plan make_spec2_plan(const HostModel& hm);
+
+struct DeviceSpec2Plan {
+    Spec2Plan plan;
+    DeviceBuffer d_lcol, d_lval, d_hcol, d_hval, d_hhid, d_hrow, d_hoff, d_amax;
+    Spec2Model view{};
+    void upload(const Spec2Plan& p, const HostModel& hm, const float* d_emis, hipStream_t s);
+};
+
 // Pinned host staging buffer (grow-only).
 template <class T>
 struct Pinned {
@@ -211,10 +229,14 @@ struct Model {
     DevicePlan paths_plan_storage;   // term-by-term plan when fast_plan is uniform
     const DevicePlan* paths_plan = nullptr;
     DeviceBuffer d_gemis, d_gstart, d_rowptr, d_col, d_val, d_rowof;  // CSR (generic, _spec)
-    // _spec products
+    // _spec products (level >= 3, or level 2 on models the on-chip kernel does not take)
     uint32_t spec_level = 0;
     uint32_t pstride = 0;
     DeviceBuffer d_mfold, d_products;
+    // _spec level 2 on chip (spec2.hip): built by spec_build(2) unless SVH_SPEC_DENSE=1
+    DeviceSpec2Plan spec2;
+    bool spec2_on = false;
+    bool spec_dense = false;  // svh_model_opts.flags & SVH_MODEL_SPEC_DENSE
 
     Model(const HostModel& h, const svh_model_opts* opts);
     ~Model();

@@ -286,6 +286,16 @@ int svh_batch_fallbacks(svh_batch_t b, uint64_t* rows) {
     });
 }
 
+int svh_pipe_variant_built(int32_t slots, int32_t waves, int32_t table_mode, int32_t* built) {
+    return guarded([&] {
+        require(built != nullptr, "null argument");
+        bool ok = false;
+        if (table_mode == 0) ok = svh::pipe_supported(slots, waves, false);
+        else ok = slots == 2 && waves == 4 && svh::pipe_tm_supported(table_mode);
+        *built = ok ? 1 : 0;
+    });
+}
+
 int svh_batch_debug_fault(svh_batch_t b, void* stream) {
     return guarded([&] {
         require(b != nullptr, "null batch");

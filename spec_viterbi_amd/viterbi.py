@@ -42,13 +42,25 @@ def pinned_empty(shape, dtype=np.float32) -> np.ndarray:
     return arr
 
 
+def _result_arrays(out, nseq: int, n: int):
+    """(scores float32 [nseq, n], best int64 [nseq]): the caller's `out` pair, checked, or new arrays."""
+    if out is None:
+        return np.empty((nseq, n), np.float32), np.empty(nseq, np.int64)
+    scores, best = out
+    if (scores.shape != (nseq, n) or scores.dtype != np.float32 or not scores.flags.c_contiguous
+            or best.shape != (nseq,) or best.dtype != np.int64 or not best.flags.c_contiguous):
+        raise ValueError("out: (float32 [nseq, n], int64 [nseq]) C-contiguous arrays expected")
+    return scores, best
+
+
 class DeviceModel:
     """An HMM resident in HBM on one device (svh_model_create)."""
 
-    def __init__(self, hmm: HMM, device: int = -1, kernel: int = _lib.SVH_KERNEL_AUTO, max_threads: int = 0):
+    def __init__(self, hmm: HMM, device: int = -1, kernel: int = _lib.SVH_KERNEL_AUTO, max_threads: int = 0,
+                 flags: int = 0):
         self.n = int(hmm.states_num)
         self.S = int(hmm.emit_num)
-        opts = _lib.svh_model_opts(device, kernel, max_threads, 0)
+        opts = _lib.svh_model_opts(device, kernel, max_threads, flags)
         h = ctypes.c_void_p()
         sc = np.ascontiguousarray(hmm.start_probabilities_cols, np.uint64)
         sv = np.ascontiguousarray(hmm.start_probabilities, np.float32)
@@ -102,17 +114,18 @@ class DeviceModel:
         `out` = (scores [nseq, n] float32, best [nseq] int64) to fill instead of new arrays;
         arrays from pinned_empty take the scores straight from the DMA engine."""
         offsets = np.ascontiguousarray(offsets, np.uint64)
-        nseq = offsets.size - 1
-        if out is not None:
-            scores, best = out
-            if (scores.shape != (nseq, self.n) or scores.dtype != np.float32 or not scores.flags.c_contiguous
-                    or best.shape != (nseq,) or best.dtype != np.int64 or not best.flags.c_contiguous):
-                raise ValueError("out: (float32 [nseq, n], int64 [nseq]) C-contiguous arrays expected")
-        else:
-            scores = np.empty((nseq, self.n), np.float32)
-            best = np.empty(nseq, np.int64)
-        pth = np.empty(int(offsets[-1] - offsets[0]) if nseq else 0, np.int32) if paths else None
         symbols = np.asarray(symbols)
+        # the C ABI takes no symbol count: check here that every sequence lies inside `symbols`
+        # (a short array or a bad offsets vector would otherwise be a native out-of-bounds read)
+        if offsets.ndim != 1 or offsets.size < 1:
+            raise ValueError("offsets: a 1-D array of nseq + 1 entries expected")
+        if symbols.ndim != 1:
+            raise ValueError("symbols: a 1-D array expected")
+        if np.any(offsets[1:] < offsets[:-1]) or int(offsets[-1]) > symbols.size:
+            raise ValueError("offsets must be non-decreasing with offsets[-1] <= symbols.size")
+        nseq = offsets.size - 1
+        scores, best = _result_arrays(out, nseq, self.n)
+        pth = np.empty(int(offsets[-1] - offsets[0]) if nseq else 0, np.int32) if paths else None
         if symbols.dtype == np.uint8:
             symbols = np.ascontiguousarray(symbols)
             fn, sp = _lib.lib.svh_viterbi_u8, _p(symbols, ctypes.POINTER(ctypes.c_uint8))
@@ -170,9 +183,11 @@ class DeviceBatch:
                                                          ctypes.c_void_p(stream or 0), ctypes.byref(fb)))
         return int(fb.value)
 
-    def read(self, stream: int | None = None, want_paths: bool = False):
-        scores = np.empty((self.nseq, self.model.n), np.float32)
-        best = np.empty(self.nseq, np.int64)
+    def read(self, stream: int | None = None, want_paths: bool = False, out=None):
+        """Scores [nseq, n] and best states [nseq] (+ paths) of the last run.  `out` = (scores,
+        best) to fill instead of new arrays (same checks as DeviceModel.viterbi_packed); arrays from
+        pinned_empty take the D2H copy directly."""
+        scores, best = _result_arrays(out, self.nseq, self.model.n)
         pth = np.empty(self.total, np.int32) if want_paths else None
         _lib.check(_lib.lib.svh_batch_read(self._h, ctypes.c_void_p(stream or 0), _p(scores, _f32), _p(best, _i64),
                                            _p(pth, _i32) if want_paths else None))

@@ -7,6 +7,7 @@ Floats are stored as IEEE-754 bit patterns (hex) so the vectors are exact.
     python tests/golden/make_golden.py            # the fixture files below
     python tests/golden/make_golden.py digests    # score_digests.json (bench workloads)
     python tests/golden/make_golden.py spec2      # + level-2 digests of every emit_50 row (config 4)
+    python tests/golden/make_golden.py scope      # scope_digests.json: every .chmm x emit_3_3500_20
 """
 from __future__ import annotations
 
@@ -53,13 +54,15 @@ def case(hmm_path, ess_path, seq_ids, levels=(), paths=True):
 def digests():
     """Per-row SHA-256 digests of the exact float32 score bytes (and of the int32 decoded paths)
     plus best states, for every sequence of the bench workloads: 2405.chmm x emit_50_3500_20
-    (configs[2]) and x covid-19 (configs[4]).  bench.py checks every rank's timed output (and the
+    (configs[2]), x covid-19 (configs[4]) and 100.chmm x emit_3_3500_20 (configs[1]).  bench.py checks every rank's timed output (and the
     gathered rows of its strong-scaling modes) against these without running the oracle."""
     import hashlib
 
-    hmm = svh.read_HMM(os.path.join(DATA, "chmm_files/2405.chmm"))
     out = {}
-    for ess in ("emit_50_3500_20.ess", "covid-19.ess"):
+    # (model, file): the headline and config-5 workloads, and config 2 (100.chmm x emit_3_3500_20)
+    for model, ess in (("2405.chmm", "emit_50_3500_20.ess"), ("2405.chmm", "covid-19.ess"),
+                       ("100.chmm", "emit_3_3500_20.ess")):
+        hmm = svh.read_HMM(os.path.join(DATA, "chmm_files", model))
         seqs = svh.read_emit_seq(os.path.join(DATA, "ess_files", ess))
         rows = []
         for seq in seqs:
@@ -67,8 +70,8 @@ def digests():
             rows.append({"length": int(seq.size), "best_state": int(best),
                          "scores_sha256": hashlib.sha256(np.asarray(scores, np.float32).tobytes()).hexdigest(),
                          "path_sha256": hashlib.sha256(np.asarray(path, np.int32).tobytes()).hexdigest()})
-        out[f"2405.chmm x {ess}"] = rows
-        print("digests", ess, len(rows))
+        out[f"{model} x {ess}"] = rows
+        print("digests", model, ess, len(rows))
     path = os.path.join(OUT, "score_digests.json")
     if os.path.exists(path):  # keep the level-2 rows (spec2_digests) in the same file
         with open(path) as f:
@@ -105,7 +108,40 @@ def spec2_digests():
     print("spec2 digests", len(rows))
 
 
+def scope_digests():
+    """The reference's semantic-equality scope (tests/test_semantic_equality.cpp:19-98): every
+    .chmm x every sequence of emit_3_3500_20.ess, non-spec (scores, best state, decoded path) and
+    _spec level 2 (scores; the oracle builds each model's S^2 dense products once), as SHA-256
+    digests in scope_digests.json.  tests/test_reference_scope_gpu.py checks the GPU against them."""
+    import glob
+    import hashlib
+
+    def sha(a, dt):
+        return hashlib.sha256(np.ascontiguousarray(a, dt).tobytes()).hexdigest()
+
+    seqs = svh.read_emit_seq(os.path.join(DATA, "ess_files/emit_3_3500_20.ess"))
+    out = {}
+    models = sorted(glob.glob(os.path.join(DATA, "chmm_files", "*.chmm")),
+                    key=lambda f: int(os.path.basename(f).split(".")[0]))
+    for f in models:
+        name = os.path.basename(f)
+        hmm = svh.read_HMM(f)
+        rows = []
+        spec2 = oracle.viterbi_spec_batch(hmm, 2, seqs)
+        for q, seq in enumerate(seqs):
+            scores, best, path = oracle.decode(hmm, seq)
+            rows.append({"length": int(seq.size), "best_state": int(best), "scores_sha256": sha(scores, np.float32),
+                         "path_sha256": sha(path, np.int32), "spec2_sha256": sha(spec2[q], np.float32)})
+        out[name] = rows
+        print("scope", name, flush=True)
+    with open(os.path.join(OUT, "scope_digests.json"), "w") as fh:
+        json.dump({"ess": "emit_3_3500_20.ess", "models": out}, fh, indent=0)
+
+
 def main():
+    if sys.argv[1:] == ["scope"]:
+        scope_digests()
+        return
     if sys.argv[1:] == ["digests"]:
         digests()
         return

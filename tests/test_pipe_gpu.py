@@ -198,6 +198,10 @@ def test_pipew_geometries(waves):
 
 @pytest.mark.parametrize("geom", [(1, 4), (1, 8), (2, 4), (2, 8)])
 def test_pipe_geometries(geom, monkeypatch):
+    """The latency plan's other geometries (1 x 4, 1 x 8, 2 x 8: built only with -DSVH_PIPE_AB_ALL,
+    AUTO plans 2 x 4) on a random chain model against the oracle."""
+    if not _lib.pipe_variant_built(geom[0], geom[1], 0 if geom != (2, 4) else 4):
+        pytest.skip(f"geometry {geom} is an A/B build's (-DSVH_PIPE_AB_ALL)")
     monkeypatch.setenv("SVH_PIPE_SM", str(geom[0]))
     monkeypatch.setenv("SVH_PIPE_WAVES", str(geom[1]))
     hmm = random_chain_hmm(1300, S=20, seed=21, n_from_m=False)
@@ -213,7 +217,9 @@ def test_pipe_table_modes(tm, monkeypatch):
     """Every step table mode of the latency plan (pipe_kernel.h TM: per-slot tables, pair tables by
     64-bit moves, indexed operands, packed feeder terms, both) on the headline rows against the
     goldens and on random chain models (ties, +inf edges, light starts, chain breaks, lengths around
-    the group / window boundaries) against the oracle."""
+    the group / window boundaries) against the oracle.  TM 1..3 are A/B builds' (-DSVH_PIPE_AB_ALL)."""
+    if not _lib.pipe_variant_built(2, 4, tm):
+        pytest.skip(f"table mode {tm} is an A/B build's (-DSVH_PIPE_AB_ALL)")
     monkeypatch.setenv("SVH_PIPE_TM", str(tm))
     import hashlib
 
