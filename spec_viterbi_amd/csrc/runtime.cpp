@@ -1183,6 +1183,10 @@ Spec2Plan make_spec2_plan(const HostModel& hm) {
     for (float e : hm.emis) nonneg = nonneg && e >= 0.0f;
     for (float e : hm.start) nonneg = nonneg && e >= 0.0f;
     sp.prune = nonneg;
+    if (H == 0) {  // no heavy rows: one padding entry each, so every upload has a source
+        sp.hrow.push_back(0);
+        sp.amax.push_back(0.0f);
+    }
     sp.ok = true;
     return sp;
 }
@@ -1196,9 +1200,9 @@ void DeviceSpec2Plan::upload(const Spec2Plan& p, const HostModel& hm, const floa
     d_hcol.upload(p.hcol.data(), p.hcol.size() * 4, s);
     d_hval.upload(p.hval.data(), p.hval.size() * 4, s);
     d_hhid.upload(p.hhid.data(), p.hhid.size() * 4, s);
-    d_hrow.upload(p.hrow.data(), std::max<size_t>(p.hrow.size(), 1) * 4, s);
+    d_hrow.upload(p.hrow.data(), p.hrow.size() * 4, s);
     d_hoff.upload(p.hoff.data(), p.hoff.size() * 4, s);
-    d_amax.upload(p.amax.data(), std::max<size_t>(p.amax.size(), 1) * 4, s);
+    d_amax.upload(p.amax.data(), p.amax.size() * 4, s);
     view.emis = d_emis;
     view.lcol = d_lcol.as<uint32_t>();
     view.lval = d_lval.as<float>();

@@ -100,7 +100,7 @@ def _neg_hmm(seed):
     tp[flip & np.isfinite(tp)] *= -0.5
     hmm.trans_probs = tp
     em = hmm.emissions.copy()
-    em[rng.random(em.shape) < 0.1] *= -1.0
+    em[(rng.random(em.shape) < 0.1) & np.isfinite(em)] *= -1.0
     hmm.emissions = em
     return hmm
 
