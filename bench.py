@@ -250,13 +250,17 @@ def pmc_counters(launch_args: list[str], kernel_prefix: str) -> dict | None:
     return out or None
 
 
-def essential_bytes_per_launch(n: int, S: int, lengths, paths: bool) -> int:
+XCDS = 8  # MI355X_MICROARCH.md: 8 XCDs, each with its own L2
+
+
+def essential_bytes_per_launch(n: int, S: int, lengths, paths: bool, xcds: int = XCDS) -> int:
     """HBM bytes a launch cannot avoid: the symbols (uint8) in, the scores (fp32) and best states
-    (int64) out, the model's folded (eb, ea) tables (S x n float pairs) read once, and with paths
+    (int64) out, the model's folded (eb, ea) tables (S x n float pairs) read once per XCD (each XCD's
+    L2 misses on them once: the workgroups that read a table are spread over all 8), and with paths
     the decoded path (int32 per observation).  SURVEY 8(d)'s streamed-CSR bytes are not this
     kernel's bound (it keeps the model and the scores on chip): reported as bytes only."""
     nseq = len(lengths)
-    return sum(lengths) + nseq * n * 4 + nseq * 8 + S * n * 8 + (4 * sum(lengths) if paths else 0)
+    return sum(lengths) + nseq * n * 4 + nseq * 8 + xcds * S * n * 8 + (4 * sum(lengths) if paths else 0)
 
 
 def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc, essential_bytes) -> dict:
@@ -333,7 +337,7 @@ def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc, essential_bytes) -> d
                    "frac_chip = the same over the whole chip (CUs x 4 SIMDs x 1/2 per cycle x 2.4 GHz); issue_frac_all = "
                    "VALU + SALU + LDS instructions over one wave's issue rate (1 per 4 cycles) on the occupied SIMDs; "
                    "hbm.essential_* = the bytes a launch cannot avoid (symbols in, scores and best states out, the "
-                   "folded tables once); hbm.measured_* the PMC bytes (FETCH_SIZE x2 + WRITE_SIZE) and their ratio to "
+                   "folded tables once per XCD); hbm.measured_* the PMC bytes (FETCH_SIZE x2 + WRITE_SIZE) and their ratio to "
                    "the essential bytes; hbm.streamed_csr_model_bytes = SURVEY 8(d)'s streamed-CSR model (47.98 "
                    "B/state-update), not a bound for a kernel that keeps the model on chip, so no rate is derived from it")
     return res
@@ -535,9 +539,11 @@ def main(argv=None):
                  else "spec_chunk+" + KERNEL_NAMES.get(plan["kernel"], "?") if args.level >= 2
                  else KERNEL_NAMES.get(plan["kernel"], "?"))
         pmc = None
-        if not args.no_pmc and world == 1 and args.level <= 1 and not args.paths and plan["kernel"] in (4, 5, 6):
+        if not args.no_pmc and world == 1 and args.level <= 1 and plan["kernel"] in (4, 5, 6):
+            # the dominant kernel's counters (with --paths: the pipelined kernel's PATHS variant, the
+            # pass's dominant kernel; its traceback and the exiting chain launch are not counted)
             largs = ["--model", args.model, "--ess", ess_name, "--replicate", str(args.replicate), "--steps", "3",
-                     "--warmup", "1"]
+                     "--warmup", "1"] + (["--paths"] if args.paths else [])
             kpref = {4: "chain_viterbi_kernel", 5: "pipe_viterbi_kernel", 6: "pipew_viterbi_kernel"}[plan["kernel"]]
             pmc = pmc_counters(largs, "void svh::(anonymous namespace)::" + kpref)
         # level >= 2 streams one dense product per chunk from HBM: those bytes are its bound

@@ -386,24 +386,32 @@ hipError_t launch_spec_chunk(const CsrModel& m, const float* products, const Spe
 // _spec level 2 on chip (spec2.hip): one persistent workgroup of kSpec2Threads per sequence runs
 // every chunk of two observations from the folded sparse matrices (no dense products).
 // Rows with at most kSpec2LightMax terms are light (their terms in registers of the thread
-// r % 1024, slot r / 1024), the others heavy (their terms spread over the threads, x = hs * 1024 +
-// t, sorted by row).  Columns are packed as m | (heavy index of m + 1) << 16 (0: m is light).
+// r % 1024, slot r / 1024); the others heavy (their terms padded to a multiple of nhs and spread
+// over consecutive threads, nhs per thread, one row per thread).  Per term two words: `a` where the
+// column's score is read in LDS (float index; bit 31: a heavy row's order-preserving key) and `b`
+// where the column's (b, v) pair list starts (bits 0..19, pair index) and which count cell holds
+// its length (bits 20..31: heavy index, H = KL for a light column, H + 1 = 0 for padding).
 constexpr uint32_t kSpec2Threads = 1024;
 constexpr uint32_t kSpec2LightMax = 4;
 struct Spec2Model {
     const float* emis;     // [S][n]
-    const uint32_t* lcol;  // [R][KL][1024] packed columns of the light rows' terms (0xFFFFFFFF: none)
-    const float* lval;     // [R][KL][1024] T^T values
-    const uint32_t* hcol;  // [NHS * 1024] packed columns of the heavy terms
-    const float* hval;     // [NHS * 1024]
-    const uint32_t* hhid;  // [NHS * 1024] heavy index of the term's row (0xFFFFFFFF: padding)
+    const uint32_t* la;    // [R][KL][1024] light terms: score address
+    const uint32_t* lb;    // [R][KL][1024] light terms: pair list
+    const float* lv;       // [R][KL][1024] light terms: T^T value (+inf: padding)
+    const uint32_t* thr;   // [1024] heavy row of the thread (H: none)
+    const uint32_t* tcp;   // [1024] pair index of that row's candidate range
+    const uint32_t* ha;    // [1024][NHS] heavy terms: score address
+    const uint32_t* hb;    // [1024][NHS] heavy terms: pair list
+    const float* hv;       // [1024][NHS] heavy terms: T^T value (+inf: padding)
     const uint32_t* hrow;  // [H] state of heavy row h
-    const uint32_t* hoff;  // [H + 1] first term of heavy row h
     const float* amax;     // [H] max over symbols and out-terms (j, p) of the finite fl(E_s[j] + T^T[j][p])
-    uint32_t n, S, H, NH;
-    uint32_t R, KL, NHS;   // instantiated sizes (rounded: 2/4, 2/4, 4/8)
+    uint32_t n, S, H, NP;  // NP: candidate pair capacity (the heavy rows' padded term counts)
+    uint32_t R, KL, NHS;   // instantiated sizes (rounded: 2/3/4, 2/4, 4/6/8)
+    uint32_t nhs;          // heavy terms per thread (<= NHS)
     uint32_t prune;        // every score >= 0: candidates pruned (spec2.hip); 0: every term kept
+    unsigned long long* stamps;  // diagnostics (-DSVH_SPEC2_DIAG builds, SVH_SPEC2_DEBUG=1): [seq][16][8]
 };
+constexpr int kSpec2Stamps = 8;
 struct Spec2Batch {
     const uint8_t* symbols;
     const uint64_t* sym_off;
@@ -413,35 +421,29 @@ struct Spec2Batch {
     uint32_t nseq;
 };
 struct Spec2Lds {
-    uint32_t v, lp, hp, cl, hacc, cmin, ccnt, eh, hoff, amax;  // offsets in floats (16-byte aligned)
+    uint32_t v, pairs, hacc, cmin, ccnt, eh, amax;  // offsets in floats (16-byte aligned)
     size_t bytes;
 };
 __host__ __device__ inline uint32_t spec2_al4(uint32_t x) { return (x + 3u) & ~3u; }
-__host__ __device__ inline Spec2Lds spec2_lds_layout(uint32_t n, uint32_t KL, uint32_t NH, uint32_t H) {
-    // v [n] | LP [n][KL] float2 | HP [NH] float2 | CL [NH] u16 | hacc [H] | cmin [2][H] | ccnt [2][H]
-    // | EH [2][2][H] | hoff [H + 1] | amax [H]
+__host__ __device__ inline Spec2Lds spec2_lds_layout(uint32_t n, uint32_t KL, uint32_t NP, uint32_t H) {
+    // v [n + 1] | pairs float2 [n KL + NP] | hacc [H + 1] | cmin [2][H + 1] | ccnt [2][H + 2]
+    // | EH [2][2][H + 1] | amax [H + 1]
     Spec2Lds L;
     uint32_t o = 0;
     L.v = o;
-    o += spec2_al4(n);
-    L.lp = o;
-    o += spec2_al4(2 * n * KL);
-    L.hp = o;
-    o += spec2_al4(2 * NH);
-    L.cl = o;
-    o += spec2_al4((NH + 1) / 2);
+    o += spec2_al4(n + 1);
+    L.pairs = o;
+    o += spec2_al4(2 * (n * KL + NP));
     L.hacc = o;
-    o += spec2_al4(H);
-    L.cmin = o;
-    o += spec2_al4(2 * H);
-    L.ccnt = o;
-    o += spec2_al4(2 * H);
-    L.eh = o;
-    o += spec2_al4(4 * H);
-    L.hoff = o;
     o += spec2_al4(H + 1);
+    L.cmin = o;
+    o += spec2_al4(2 * (H + 1));
+    L.ccnt = o;
+    o += spec2_al4(2 * (H + 2));
+    L.eh = o;
+    o += spec2_al4(4 * (H + 1));
     L.amax = o;
-    o += spec2_al4(H);
+    o += spec2_al4(H + 1);
     L.bytes = (size_t)o * 4;
     return L;
 }

@@ -105,6 +105,15 @@ __device__ __forceinline__ void wait_vmcnt() {
 #define SVH_PIPE_XL 1
 #endif
 
+// Diagnostic ablation (-DSVH_PIPE_NOWAIT, timing only, wrong results): every exchange operation
+// runs, but no wait on a neighbour does (counts, flow control, granule tags and progress words are
+// taken as ready): the rate of a wave when no neighbour ever holds it up.
+#ifdef SVH_PIPE_NOWAIT
+constexpr bool kNoWait = true;
+#else
+constexpr bool kNoWait = false;
+#endif
+
 // One lane's LDS store of a wave-uniform word (a wave's count): EXEC narrowed to lane 0 inside the
 // asm (no divergent branch in the compiler's view).  Measured and not kept (round 4): every lane
 // storing, lanes 1..63 into a sink of their own (no EXEC writes), within noise.
@@ -757,6 +766,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         };
         // wait until the previous wave has published observations < need
         auto wait_prev = [&](uint32_t need) {
+            if (kNoWait) return;
             while ((uint32_t)uniform((int)lds_ld32(cnt_w - 1)) < need) {
                 if (dbg) ++dg[3];
                 if (give_up()) break;
@@ -765,6 +775,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         };
         // flow control: the next wave has consumed observations < need
         auto wait_next = [&](uint32_t need) {
+            if (kNoWait) return;
             while ((int)uniform((int)lds_ld32(cnt_w + 1)) < (int)need) {
                 if (dbg) ++dg[4];
                 if (give_up()) break;
@@ -784,7 +795,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 const bool need = lane < 8u && sl + 1u < len;
                 const uint64_t* p = gin + (sl & (kGR - 1));
                 uint64_t gv = g_ld64(p);
-                while (__builtin_amdgcn_ballot_w64(need && (uint32_t)(gv >> 32) != gtag(ep, sl)) != 0) {
+                while (!kNoWait && __builtin_amdgcn_ballot_w64(need && (uint32_t)(gv >> 32) != gtag(ep, sl)) != 0) {
                     if (dbg) ++dg[5];
                     if (give_up()) break;
                     __builtin_amdgcn_s_sleep(1);
@@ -801,6 +812,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             return (uint64_t)(uint32_t)uniform((int)(uint32_t)c) | ((uint64_t)(uint32_t)uniform((int)(uint32_t)(c >> 32)) << 32);
         };
         auto wait_cons = [&](uint32_t need) {
+            if (kNoWait) return;
             uint64_t c = g_ld64(cons_out);
             while (!cons_ok(uni64(c), need)) {
                 if (dbg) ++dg[6];
@@ -929,7 +941,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         if constexpr (SRC == 2) {
                             wait_vmcnt<kGpf - 1>();  // gq[j]: kGpf - 1 later loads in flight
                             uint64_t gv = gq[j % kGpf];
-                            while (__builtin_amdgcn_ballot_w64((uint32_t)(gv >> 32) != gtag(ep, tg)) != 0) {
+                            while (!kNoWait && __builtin_amdgcn_ballot_w64((uint32_t)(gv >> 32) != gtag(ep, tg)) != 0) {
                                 if (dbg) ++dg[5];
                                 if (give_up()) break;
                                 __builtin_amdgcn_s_sleep(1);
@@ -1000,7 +1012,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         put_cnt(tg + 8);
                         if constexpr (SRC == 1) {  // the next group's boundary vector (valid if next_ok)
                             if constexpr (SVH_PIPE_LDSX) asm volatile("" : "+v"(pc_rd));
-                            next_ok = (uint32_t)uniform((int)pc_rd) >= tg + 16;
+                            next_ok = kNoWait || (uint32_t)uniform((int)pc_rd) >= tg + 16;
                             asm volatile("" ::: "memory");
                             bv_next = ring_prev[ring_idx(((8 * j + 8) & (kR - 1)) + (lane & 7u), 63)];
                         }

@@ -1122,51 +1122,81 @@ Spec2Plan make_spec2_plan(const HostModel& hm) {
     const uint32_t n = hm.n, S = hm.S, T = kSpec2Threads;
     if (n == 0 || n > 65535 || n > 4 * T) return sp;
     std::vector<int32_t> hid(n, -1);
-    uint32_t klmax = 1, NH = 0;
+    uint32_t klmax = 1;
+    std::vector<uint32_t> deg;
     for (uint32_t r = 0; r < n; ++r) {
-        const uint32_t deg = hm.rowptr[r + 1] - hm.rowptr[r];
-        if (deg > kSpec2LightMax) {
+        const uint32_t d = hm.rowptr[r + 1] - hm.rowptr[r];
+        if (d > kSpec2LightMax) {
             hid[r] = (int32_t)sp.hrow.size();
             sp.hrow.push_back(r);
-            NH += deg;
+            deg.push_back(d);
         } else {
-            klmax = std::max(klmax, deg);
+            klmax = std::max(klmax, d);
         }
     }
     const uint32_t H = (uint32_t)sp.hrow.size();
+    if (H + 2 > T) return sp;
+    // heavy terms per thread: the fewest (<= 8) whose padded rows fit the 1024 threads
+    uint32_t nhs = 0;
+    for (uint32_t c = 1; c <= 8 && !nhs; ++c) {
+        uint64_t threads = 0;
+        for (uint32_t d : deg) threads += (d + c - 1) / c;
+        if (threads <= T) nhs = c;
+    }
+    if (H && !nhs) return sp;
+    if (!nhs) nhs = 1;
+    sp.nhs = nhs;
     sp.R = spec2_round_r((n + T - 1) / T);
     sp.KL = spec2_round_kl(klmax);
-    sp.NHS = spec2_round_nhs(std::max<uint32_t>((NH + T - 1) / T, 1));
-    if (!sp.R || !sp.KL || !sp.NHS || H > T || NH > 65535) return sp;
-    if (spec2_lds_layout(n, sp.KL, NH, H).bytes > kMaxLdsBytes) return sp;
-    auto packed = [&](uint32_t m) { return m | ((uint32_t)(hid[m] + 1) << 16); };
+    sp.NHS = spec2_round_nhs(nhs);
+    if (!sp.R || !sp.KL || !sp.NHS) return sp;
+    std::vector<uint32_t> cpoff(H + 1, 0);  // candidate range of each heavy row (its padded term count)
+    for (uint32_t h = 0; h < H; ++h) cpoff[h + 1] = cpoff[h] + (deg[h] + nhs - 1) / nhs * nhs;
+    sp.NP = cpoff[H];
+    const Spec2Lds L = spec2_lds_layout(n, sp.KL, sp.NP, H);
+    if (L.bytes > kMaxLdsBytes || n * sp.KL + sp.NP >= (1u << 20)) return sp;
     sp.H = H;
-    sp.NH = NH;
-    sp.lcol.assign((size_t)sp.R * sp.KL * T, 0xFFFFFFFFu);
-    sp.lval.assign((size_t)sp.R * sp.KL * T, kInfH);
+    // the two words of a term whose column is m (spec2.hip): score address, pair list
+    const uint32_t pad_a = L.v + n, pad_b = (H + 1) << 20;
+    auto word_a = [&](uint32_t m) { return hid[m] < 0 ? L.v + m : (L.hacc + (uint32_t)hid[m]) | 0x80000000u; };
+    auto word_b = [&](uint32_t m) {
+        return hid[m] < 0 ? (m * sp.KL) | (H << 20) : (n * sp.KL + cpoff[hid[m]]) | ((uint32_t)hid[m] << 20);
+    };
+    sp.la.assign((size_t)sp.R * sp.KL * T, pad_a);
+    sp.lb.assign((size_t)sp.R * sp.KL * T, pad_b);
+    sp.lv.assign((size_t)sp.R * sp.KL * T, kInfH);
     for (uint32_t r = 0; r < n; ++r) {
         if (hid[r] >= 0) continue;
         const uint32_t s = r / T, t = r % T;
         for (uint32_t e = hm.rowptr[r], k = 0; e < hm.rowptr[r + 1]; ++e, ++k) {
-            sp.lcol[((size_t)s * sp.KL + k) * T + t] = packed(hm.col[e]);
-            sp.lval[((size_t)s * sp.KL + k) * T + t] = hm.val[e];
+            const size_t i = ((size_t)s * sp.KL + k) * T + t;
+            sp.la[i] = word_a(hm.col[e]);
+            sp.lb[i] = word_b(hm.col[e]);
+            sp.lv[i] = hm.val[e];
         }
     }
-    sp.hcol.assign((size_t)sp.NHS * T, 0xFFFFFFFFu);
-    sp.hval.assign((size_t)sp.NHS * T, kInfH);
-    sp.hhid.assign((size_t)sp.NHS * T, 0xFFFFFFFFu);
-    sp.hoff.assign(H + 1, 0);
-    uint32_t x = 0;
+    sp.thr.assign(T, H);
+    sp.tcp.assign(T, 0);
+    sp.ha.assign((size_t)T * sp.NHS, pad_a);
+    sp.hb.assign((size_t)T * sp.NHS, pad_b);
+    sp.hv.assign((size_t)T * sp.NHS, kInfH);
+    uint32_t t = 0;
     for (uint32_t h = 0; h < H; ++h) {
         const uint32_t r = sp.hrow[h];
-        sp.hoff[h] = x;
-        for (uint32_t e = hm.rowptr[r]; e < hm.rowptr[r + 1]; ++e, ++x) {
-            sp.hcol[x] = packed(hm.col[e]);
-            sp.hval[x] = hm.val[e];
-            sp.hhid[x] = h;
+        for (uint32_t e = hm.rowptr[r], k = 0; e < hm.rowptr[r + 1]; ++e, ++k) {
+            const uint32_t tt = t + k / nhs, hs = k % nhs;
+            const size_t i = (size_t)tt * sp.NHS + hs;
+            sp.ha[i] = word_a(hm.col[e]);
+            sp.hb[i] = word_b(hm.col[e]);
+            sp.hv[i] = hm.val[e];
         }
+        const uint32_t nt = (deg[h] + nhs - 1) / nhs;
+        for (uint32_t k = 0; k < nt; ++k) {
+            sp.thr[t + k] = h;
+            sp.tcp[t + k] = n * sp.KL + cpoff[h];
+        }
+        t += nt;
     }
-    sp.hoff[H] = x;
     // a of the terms (j, p) with p heavy, over every symbol: fl(E_s[j] + T^T[j][p]) (float adds)
     sp.amax.assign(H, 0.0f);
     bool nonneg = true;
@@ -1195,31 +1225,61 @@ void DeviceSpec2Plan::upload(const Spec2Plan& p, const HostModel& hm, const floa
     plan = p;
     std::memset(&view, 0, sizeof(view));
     if (!p.ok) return;
-    d_lcol.upload(p.lcol.data(), p.lcol.size() * 4, s);
-    d_lval.upload(p.lval.data(), p.lval.size() * 4, s);
-    d_hcol.upload(p.hcol.data(), p.hcol.size() * 4, s);
-    d_hval.upload(p.hval.data(), p.hval.size() * 4, s);
-    d_hhid.upload(p.hhid.data(), p.hhid.size() * 4, s);
+    d_la.upload(p.la.data(), p.la.size() * 4, s);
+    d_lb.upload(p.lb.data(), p.lb.size() * 4, s);
+    d_lv.upload(p.lv.data(), p.lv.size() * 4, s);
+    d_thr.upload(p.thr.data(), p.thr.size() * 4, s);
+    d_tcp.upload(p.tcp.data(), p.tcp.size() * 4, s);
+    d_ha.upload(p.ha.data(), p.ha.size() * 4, s);
+    d_hb.upload(p.hb.data(), p.hb.size() * 4, s);
+    d_hv.upload(p.hv.data(), p.hv.size() * 4, s);
     d_hrow.upload(p.hrow.data(), p.hrow.size() * 4, s);
-    d_hoff.upload(p.hoff.data(), p.hoff.size() * 4, s);
     d_amax.upload(p.amax.data(), p.amax.size() * 4, s);
     view.emis = d_emis;
-    view.lcol = d_lcol.as<uint32_t>();
-    view.lval = d_lval.as<float>();
-    view.hcol = d_hcol.as<uint32_t>();
-    view.hval = d_hval.as<float>();
-    view.hhid = d_hhid.as<uint32_t>();
+    view.la = d_la.as<uint32_t>();
+    view.lb = d_lb.as<uint32_t>();
+    view.lv = d_lv.as<float>();
+    view.thr = d_thr.as<uint32_t>();
+    view.tcp = d_tcp.as<uint32_t>();
+    view.ha = d_ha.as<uint32_t>();
+    view.hb = d_hb.as<uint32_t>();
+    view.hv = d_hv.as<float>();
     view.hrow = d_hrow.as<uint32_t>();
-    view.hoff = d_hoff.as<uint32_t>();
     view.amax = d_amax.as<float>();
     view.n = hm.n;
     view.S = hm.S;
     view.H = p.H;
-    view.NH = p.NH;
+    view.NP = p.NP;
     view.R = p.R;
     view.KL = p.KL;
     view.NHS = p.NHS;
+    view.nhs = p.nhs;
     view.prune = p.prune ? 1u : 0u;
+    if (const char* e = std::getenv("SVH_SPEC2_DEBUG"); e && std::atoi(e)) {  // diagnostics only
+        d_stamps.alloc((size_t)4096 * 16 * kSpec2Stamps * 8);
+        hip_check(hipMemsetAsync(d_stamps.ptr, 0, d_stamps.bytes, s), "stamps");
+        view.stamps = d_stamps.as<unsigned long long>();
+    }
+}
+
+void DeviceSpec2Plan::report_stamps(uint32_t nseq) const {
+    if (!view.stamps) return;
+    nseq = std::min<uint32_t>(nseq, 4096);
+    std::vector<unsigned long long> h((size_t)nseq * 16 * kSpec2Stamps);
+    if (hipMemcpy(h.data(), view.stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    double sum[kSpec2Stamps] = {};
+    double chunks = 0;
+    for (uint32_t q = 0; q < nseq; ++q)
+        for (uint32_t w = 0; w < 16; ++w) {
+            const unsigned long long* r = h.data() + ((size_t)q * 16 + w) * kSpec2Stamps;
+            for (int k = 0; k < 7; ++k) sum[k] += (double)r[k];
+            chunks += (double)r[7];
+        }
+    if (chunks <= 0) return;
+    std::fprintf(stderr, "spec2 cycles per chunk and wave (s_memtime): phase1 %.0f bar1 %.0f phase1b %.0f bar2 %.0f "
+                         "phase2 %.0f bar3 %.0f loop %.0f (%.0f chunks x waves)\n",
+                 sum[0] / chunks, sum[1] / chunks, sum[2] / chunks, sum[3] / chunks, sum[4] / chunks, sum[5] / chunks,
+                 sum[6] / chunks, chunks);
 }
 
 void Model::spec_build(uint32_t level, hipStream_t s) {
@@ -1692,6 +1752,10 @@ void Batch::run(uint32_t level, hipStream_t s) {
             sb.v = vb;
             sb.nseq = nseq;
             hip_check(launch_spec2(model->spec2.view, sb, s), "spec2 kernel");
+            if (model->spec2.view.stamps) {
+                hip_check(hipStreamSynchronize(s), "spec2 stamps");
+                model->spec2.report_stamps(nseq);
+            }
         }
         SpecChunkBatch cb;
         cb.symbols = fb.symbols;

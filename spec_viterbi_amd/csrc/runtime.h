@@ -161,16 +161,17 @@ struct DevicePipePlan {
 struct Spec2Plan {
     bool ok = false;
     bool prune = false;
-    uint32_t R = 0, KL = 0, NHS = 0, H = 0, NH = 0;
-    std::vector<uint32_t> lcol, hcol, hhid, hrow, hoff;
-    std::vector<float> lval, hval, amax;
+    uint32_t R = 0, KL = 0, NHS = 0, nhs = 0, H = 0, NP = 0;
+    std::vector<uint32_t> la, lb, thr, tcp, ha, hb, hrow;
+    std::vector<float> lv, hv, amax;
 };
 Spec2Plan make_spec2_plan(const HostModel& hm);
 
 struct DeviceSpec2Plan {
     Spec2Plan plan;
-    DeviceBuffer d_lcol, d_lval, d_hcol, d_hval, d_hhid, d_hrow, d_hoff, d_amax;
+    DeviceBuffer d_la, d_lb, d_lv, d_thr, d_tcp, d_ha, d_hb, d_hv, d_hrow, d_amax, d_stamps;
     Spec2Model view{};
+    void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_SPEC2_DEBUG, -DSVH_SPEC2_DIAG builds)
     void upload(const Spec2Plan& p, const HostModel& hm, const float* d_emis, hipStream_t s);
 };
 

@@ -26,13 +26,19 @@
 // A model with any negative score runs with theta = +inf (every term a candidate): still (1),
 // exactly, just without the pruning.
 //
-// Per chunk (symbols s1 = seq[1+2c], s2 = seq[2+2c]), three barriers:
-//   1  light rows p: pairs LP[p][k] = (b, v_m) = (fl(E_s1[p] + T^T[p][m_k]), v[m_k]);
-//      heavy terms x of row p: HP[x] = (b, v_m), c_f = fl(b + v_m), a per-row minimum (LDS atomic);
-//   1b heavy terms: candidates c_f <= theta appended to CL[row's range] (wave-aggregated atomics);
-//   2  light rows j: v'[j] = min over its terms p of the loop over LP[p] (light p) or CL[p] (heavy
-//      p); heavy terms (j, p): the same per term, then a per-row minimum into hacc[j].
-// Scores of heavy rows live in hacc (order-preserving keys, LDS ds_min_u32), light rows in vl.
+// Data on chip: the scores of the light rows (vl) and of the heavy rows (hacc: order-preserving
+// keys, so the per-row minima are ds_min_u32); one array of (b, v_m) pairs: per light row p its KL
+// terms' pairs (LP), per heavy row its candidates (CP).  Every term carries two precomputed words:
+// where its column's score is read (phase 1) and where its column's pair list starts plus the
+// cell holding that list's length (phase 2: KL for a light column, the candidate count for a heavy
+// one, 0 for a padding term), so no step branches on the kind of a column.
+// Per chunk (symbols s1 = seq[1+2c], s2 = seq[2+2c]), three barriers (LDS only: the next chunk's
+// emission loads stay in flight across them):
+//   1  light rows p: LP[p][k] = (fl(E_s1[p] + T^T[p][m_k]), v[m_k]); heavy terms of row p: (b, v_m)
+//      in registers, c_f = fl(b + v_m), the row's minimum c_f (one wave reduction + LDS atomic);
+//   1b heavy terms: the candidates' pairs (c_f <= theta) appended to CP[row];
+//   2  light rows j: v'[j] = min over its terms p of the loop over p's pairs; heavy terms (j, p):
+//      the same per term, then the row's minimum into hacc[j].
 #include "device_common.h"
 #include "kernels.h"
 
@@ -43,7 +49,6 @@ using namespace dev;
 namespace {
 
 constexpr uint32_t kS2Threads = kSpec2Threads;
-constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // order-preserving key of a float (unsigned order == float order, -0 below +0): ds_min_u32 on keys
 // is a float minimum with no denormal or signed-zero ambiguity
@@ -66,23 +71,34 @@ __device__ __forceinline__ float theta_of(float cmin, float amax, bool prune) {
     return cmin + d;
 }
 
+// Diagnostics (-DSVH_SPEC2_DIAG, then SVH_SPEC2_DEBUG=1): shader cycles per wave spent in phase 1,
+// the barrier after it, phase 1b, its barrier, phase 2, its barrier, and the whole loop.
+#ifdef SVH_SPEC2_DIAG
+#define S2_T(k)                                                     \
+    do {                                                            \
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(); \
+        dg[k] += t1 - t0;                                           \
+        t0 = t1;                                                    \
+    } while (0)
+#else
+#define S2_T(k) ((void)0)
+#endif
+
 template <int R, int KL, int NHS>
 __global__ __launch_bounds__(kS2Threads) void spec2_kernel(Spec2Model m, Spec2Batch b) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const uint32_t n = m.n, H = m.H, NH = m.NH;
+    const uint32_t n = m.n, H = m.H, nhs = m.nhs;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint32_t q = blockIdx.x;
-    const Spec2Lds L = spec2_lds_layout(n, KL, NH, H);
-    float* vl = lds + L.v;
-    float2* LP = reinterpret_cast<float2*>(lds + L.lp);
-    float2* HP = reinterpret_cast<float2*>(lds + L.hp);
-    uint16_t* CL = reinterpret_cast<uint16_t*>(lds + L.cl);
-    uint32_t* hacc = reinterpret_cast<uint32_t*>(lds + L.hacc);
-    uint32_t* cmin = reinterpret_cast<uint32_t*>(lds + L.cmin);  // [2][H] keys
-    uint32_t* ccnt = reinterpret_cast<uint32_t*>(lds + L.ccnt);  // [2][H]
-    float* EH = lds + L.eh;                                      // [2 parity][2 (s1, s2)][H]
-    uint32_t* hoff = reinterpret_cast<uint32_t*>(lds + L.hoff);  // [H + 1]
-    float* amax = lds + L.amax;                                  // [H]
+    const Spec2Lds L = spec2_lds_layout(n, KL, m.NP, H);
+    float* vl = lds + L.v;                                       // [n + 1]: vl[n] = +inf
+    float2* PR = reinterpret_cast<float2*>(lds + L.pairs);       // LP [n][KL] | CP [NP]
+    uint32_t* hacc = reinterpret_cast<uint32_t*>(lds + L.hacc);  // [H + 1] keys (H: padding row)
+    uint32_t* cmin = reinterpret_cast<uint32_t*>(lds + L.cmin);  // [2][H + 1] keys
+    uint32_t* ccnt = reinterpret_cast<uint32_t*>(lds + L.ccnt);  // [2][H + 2]: H = KL, H + 1 = 0
+    float* EH = lds + L.eh;                                      // [2 parity][2 (s1, s2)][H + 1]
+    float* amax = lds + L.amax;                                  // [H + 1]
+    const uint32_t H1 = H + 1, H2 = H + 2;
 
     const uint32_t nch = b.nchunks[q];
     float* vg = b.v + (size_t)q * n;
@@ -91,38 +107,46 @@ __global__ __launch_bounds__(kS2Threads) void spec2_kernel(Spec2Model m, Spec2Ba
     const bool prune = m.prune != 0;
 
     for (uint32_t j = t; j < n; j += kS2Threads) vl[j] = vg[j];
-    for (uint32_t h = t; h < H; h += kS2Threads) {
-        hoff[h] = m.hoff[h];
-        amax[h] = m.amax[h];
-        cmin[h] = cmin[H + h] = okey(kInf);
-        ccnt[h] = ccnt[H + h] = 0;
+    if (t == 0) vl[n] = kInf;
+    for (uint32_t h = t; h <= H; h += kS2Threads) {
+        amax[h] = h < H ? m.amax[h] : 0.0f;
+        cmin[h] = cmin[H1 + h] = okey(kInf);
+        hacc[h] = okey(h < H ? vg[m.hrow[h]] : kInf);
+        EH[h] = EH[H1 + h] = EH[2 * H1 + h] = EH[3 * H1 + h] = kInf;
     }
-    if (t == 0) hoff[H] = m.hoff[H];
+    for (uint32_t h = t; h < H2; h += kS2Threads) ccnt[h] = ccnt[H2 + h] = h == H ? (uint32_t)KL : 0u;
 
-    // the thread's light rows r = s * 1024 + t: terms (packed m | (heavy index of m + 1) << 16)
-    uint32_t lc[R][KL];
+    // light rows r = s * 1024 + t: per term the score address (la), the pair list (lb: base | cell
+    // << 20) and T^T's value
+    uint32_t la[R][KL], lb[R][KL];
     float lv[R][KL];
 #pragma unroll
     for (int s = 0; s < R; ++s)
 #pragma unroll
         for (int k = 0; k < KL; ++k) {
-            lc[s][k] = m.lcol[((size_t)s * KL + k) * kS2Threads + t];
-            lv[s][k] = m.lval[((size_t)s * KL + k) * kS2Threads + t];
+            const size_t i = ((size_t)s * KL + k) * kS2Threads + t;
+            la[s][k] = m.la[i];
+            lb[s][k] = m.lb[i];
+            lv[s][k] = m.lv[i];
         }
-    // the thread's heavy terms x = hs * 1024 + t (sorted by row), their row's heavy index
-    uint32_t hc[NHS], hh[NHS];
+    // heavy terms: this thread's row (H: none) and its nhs terms (the row's terms padded to a
+    // multiple of nhs, so a thread's terms never straddle two rows)
+    const uint32_t hr = m.thr[t];
+    const uint32_t hcp = m.tcp[t];  // the row's CP range (pair index)
+    uint32_t ha[NHS], hb[NHS];
     float hv[NHS];
-    uint32_t uni = 0;  // bit hs: the wave's 64 terms of slot hs all belong to one heavy row
 #pragma unroll
     for (int hs = 0; hs < NHS; ++hs) {
-        hc[hs] = m.hcol[(size_t)hs * kS2Threads + t];
-        hv[hs] = m.hval[(size_t)hs * kS2Threads + t];
-        hh[hs] = m.hhid[(size_t)hs * kS2Threads + t];
-        const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)hh[hs], 0);
-        const uint32_t h63 = (uint32_t)__builtin_amdgcn_readlane((int)hh[hs], 63);
-        if (h0 == h63 && h0 < H) uni |= 1u << hs;
+        const size_t i = (size_t)t * NHS + hs;
+        ha[hs] = m.ha[i];
+        hb[hs] = m.hb[i];
+        hv[hs] = m.hv[i];
     }
-    const uint32_t hrow_t = t < H ? m.hrow[t] : 0;  // H <= kS2Threads (host check)
+    const uint32_t hr0 = (uint32_t)__builtin_amdgcn_readlane((int)hr, 0);
+    const uint32_t hr63 = (uint32_t)__builtin_amdgcn_readlane((int)hr, 63);
+    const bool hwave = __builtin_amdgcn_ballot_w64(hr < H) != 0;  // the wave has heavy terms
+    const bool huni = hr0 == hr63 && hr0 < H;                     // ... all of one row
+    const uint32_t hrow_t = t < H ? m.hrow[t] : 0;                // H <= kS2Threads - 2 (host check)
 
     // symbols in per-wave VGPR windows: lane l holds bytes wbase + 4l .. +3 (256 per window)
     auto load_win = [&](uint32_t base) -> uint32_t {
@@ -130,13 +154,13 @@ __global__ __launch_bounds__(kS2Threads) void spec2_kernel(Spec2Model m, Spec2Ba
         return off + 4 <= len + kSymPad ? *reinterpret_cast<const uint32_t*>(sym + off) : 0u;
     };
     uint32_t wbase = 0, wcur = load_win(0), wnext = load_win(256);
-    auto sym_at = [&](uint32_t i) -> uint32_t {  // i >= wbase (uniform)
+    auto sym_at = [&](uint32_t i) -> uint32_t {  // wbase <= i < wbase + 512 (uniform)
         const uint32_t off = i - wbase;
         const uint32_t word = off < 256 ? (uint32_t)__builtin_amdgcn_readlane((int)wcur, (int)(off >> 2))
                                         : (uint32_t)__builtin_amdgcn_readlane((int)wnext, (int)((off - 256) >> 2));
         return (word >> ((off & 3u) * 8)) & 0xFFu;
     };
-    auto advance_win = [&](uint32_t i) {  // keep i (and i + 3) inside the two windows
+    auto advance_win = [&](uint32_t i) {  // keep i and i + 1 inside the two windows
         if (i >= wbase + 256) {
             wbase += 256;
             wcur = wnext;
@@ -144,10 +168,11 @@ __global__ __launch_bounds__(kS2Threads) void spec2_kernel(Spec2Model m, Spec2Ba
         }
     };
 
-    // E of the thread's light rows for the current chunk (e1, e2) and the next (n1, n2)
+    // E of the thread's light rows for the current chunk (e1, e2) and the next (n1, n2); t < H: E of
+    // heavy row t for the next chunk (g1, g2), written to EH at the end of the chunk
     float e1[R], e2[R], n1[R], n2[R];
-    float hn1 = kInf, hn2 = kInf;  // t < H: E of heavy row t for the next chunk
-    auto fetch_e = [&](uint32_t c, float (&f1)[R], float (&f2)[R], float& g1, float& g2) {
+    float g1 = kInf, g2 = kInf;
+    auto fetch_e = [&](uint32_t c, float (&f1)[R], float (&f2)[R]) {
         const uint32_t s1 = sym_at(1 + 2 * c), s2 = sym_at(2 + 2 * c);
         const float* E1 = m.emis + (size_t)s1 * n;
         const float* E2 = m.emis + (size_t)s2 * n;
@@ -163,162 +188,155 @@ __global__ __launch_bounds__(kS2Threads) void spec2_kernel(Spec2Model m, Spec2Ba
         }
     };
     if (nch) {
-        fetch_e(0, e1, e2, hn1, hn2);
+        fetch_e(0, e1, e2);
         if (t < H) {
-            EH[t] = hn1;
-            EH[H + t] = hn2;
+            EH[t] = g1;
+            EH[H1 + t] = g2;
         }
     }
     __syncthreads();
-    for (uint32_t h = t; h < H; h += kS2Threads) hacc[h] = okey(vl[m.hrow[h]]);
-    __syncthreads();
 
-    auto vread = [&](uint32_t c) -> float {  // score of the packed column c (light: vl, heavy: hacc)
-        const uint32_t mh = c >> 16;
-        return mh ? okey_val(hacc[mh - 1]) : vl[c & 0xFFFFu];
+    // score of a term's column: light -> vl, heavy -> hacc (a key), padding -> vl[n] = +inf
+    auto vread = [&](uint32_t a) -> float {
+        const uint32_t raw = __builtin_bit_cast(uint32_t, lds[a & 0x7FFFFFFFu]);
+        return (a & 0x80000000u) ? okey_val(raw) : __builtin_bit_cast(float, raw);
     };
-    // min over p's terms of fl(fl(a + b) + v): light p from LP, heavy p from its candidates
-    auto inner = [&](uint32_t pc, float a, uint32_t par) -> float {
+    // min over the column's pairs of fl(fl(a + b) + v): a light column's KL pairs with 16-byte
+    // reads (no count), a heavy column's candidates (count cell), a padding term none
+    auto apply = [&](uint32_t pb, float a, const uint32_t* cc) -> float {
+        const uint32_t base = pb & 0xFFFFFu, cell = pb >> 20;
         float acc = kInf;
-        const uint32_t ph = pc >> 16;
-        if (ph == 0) {
-            const uint32_t p = pc & 0xFFFFu;
-            if constexpr (KL == 2) {
-                const float4 pr = *reinterpret_cast<const float4*>(LP + (size_t)p * 2);
-                acc = fminf((a + pr.x) + pr.y, (a + pr.z) + pr.w);
-            } else {
+        if (cell == H) {
 #pragma unroll
-                for (int k = 0; k < KL; k += 2) {
-                    const float4 pr = *reinterpret_cast<const float4*>(LP + (size_t)p * KL + k);
-                    acc = fminf(acc, fminf((a + pr.x) + pr.y, (a + pr.z) + pr.w));
-                }
+            for (int k = 0; k < KL; k += 2) {
+                const float4 pr = *reinterpret_cast<const float4*>(PR + base + k);
+                acc = fminf(acc, fminf((a + pr.x) + pr.y, (a + pr.z) + pr.w));
             }
         } else {
-            const uint32_t h = ph - 1;
-            const uint32_t cnt = ccnt[par * H + h], base = hoff[h];
+            const uint32_t cnt = cc[cell];
+#pragma nounroll
             for (uint32_t i = 0; i < cnt; ++i) {
-                const float2 pr = HP[CL[base + i]];
+                const float2 pr = PR[base + i];
                 acc = fminf(acc, (a + pr.x) + pr.y);
             }
         }
         return acc;
     };
 
-    float cv[NHS];
+    float cb[NHS], cm[NHS], cv[NHS];  // heavy terms: (b, v_m) and c_f, phase 1 -> 1b
+#ifdef SVH_SPEC2_DIAG
+    unsigned long long dg[kSpec2Stamps] = {};
+    unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long tloop = t0;
+#endif
     for (uint32_t c = 0; c < nch; ++c) {
-        // opaque per iteration: the addresses derived from the terms are recomputed in the chunk
-        // (a few VALU) instead of being hoisted out of the loop into ~100 more VGPRs (spills)
+        // opaque per iteration: what is derived from the term words is recomputed in the chunk
+        // instead of being hoisted out of the loop into more VGPRs (spills)
 #pragma unroll
         for (int s = 0; s < R; ++s)
 #pragma unroll
-            for (int k = 0; k < KL; ++k) asm volatile("" : "+v"(lc[s][k]));
+            for (int k = 0; k < KL; ++k) asm volatile("" : "+v"(la[s][k]), "+v"(lb[s][k]));
 #pragma unroll
-        for (int hs = 0; hs < NHS; ++hs) asm volatile("" : "+v"(hc[hs]), "+v"(hh[hs]));
+        for (int hs = 0; hs < NHS; ++hs) asm volatile("" : "+v"(ha[hs]), "+v"(hb[hs]));
         const uint32_t par = c & 1u;
-        const float* EHc = EH + par * 2 * H;
+        const float* EHc = EH + par * 2 * H1;
+        const uint32_t* ccp = ccnt + par * H2;
         const bool more = c + 1 < nch;
         if (more) {
             advance_win(2 * c + 3);
-            fetch_e(c + 1, n1, n2, hn1, hn2);
+            fetch_e(c + 1, n1, n2);
         }
         // ---- phase 1: (b, v_m) pairs; heavy c_f and its per-row minimum
 #pragma unroll
         for (int s = 0; s < R; ++s) {
+            if (s * kS2Threads + w * 64 >= n) continue;  // wave-uniform
             const uint32_t r = s * kS2Threads + t;
+            float2 pp[KL];
+#pragma unroll
+            for (int k = 0; k < KL; ++k) pp[k] = make_float2(e1[s] + lv[s][k], vread(la[s][k]));
             if (r < n) {
 #pragma unroll
-                for (int k = 0; k < KL; ++k) {
-                    const uint32_t cc = lc[s][k];
-                    LP[(size_t)r * KL + k] = cc == kNone ? make_float2(kInf, kInf)
-                                                         : make_float2(e1[s] + lv[s][k], vread(cc));
+                for (int k = 0; k < KL; k += 2)
+                    *reinterpret_cast<float4*>(PR + (size_t)r * KL + k) = make_float4(pp[k].x, pp[k].y, pp[k + 1].x, pp[k + 1].y);
+            }
+        }
+        if (hwave) {
+            const float eh1 = EHc[hr];
+            float part = kInf;
+#pragma unroll
+            for (int hs = 0; hs < NHS; ++hs) {
+                cv[hs] = kInf;
+                if ((uint32_t)hs >= nhs) continue;  // uniform
+                cb[hs] = eh1 + hv[hs];
+                cm[hs] = vread(ha[hs]);
+                cv[hs] = cb[hs] + cm[hs];
+                part = fminf(part, cv[hs]);
+            }
+            if (huni) {
+                part = wave_min63(part);
+                if (lane == 63) lds_min_u32(cmin + par * H1 + hr, okey(part));
+            } else {
+                lds_min_u32(cmin + par * H1 + hr, okey(part));
+            }
+        }
+        S2_T(0);
+        lds_barrier();
+        S2_T(1);
+        // ---- phase 1b: the candidates' pairs; resets for the next chunk
+        if (hwave) {
+            const float th = theta_of(okey_val(cmin[par * H1 + hr]), amax[hr], prune);
+            uint32_t k = 0;
+#pragma unroll
+            for (int hs = 0; hs < NHS; ++hs)
+                if ((uint32_t)hs < nhs) k += (hr < H && cv[hs] <= th) ? 1u : 0u;
+            if (__builtin_amdgcn_ballot_w64(k != 0)) {
+                if (k) {
+                    uint32_t pos = hcp + __hip_atomic_fetch_add(ccnt + par * H2 + hr, k, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+                    for (int hs = 0; hs < NHS; ++hs)
+                        if ((uint32_t)hs < nhs && cv[hs] <= th) PR[pos++] = make_float2(cb[hs], cm[hs]);
                 }
             }
         }
-#pragma unroll
-        for (int hs = 0; hs < NHS; ++hs) {
-            cv[hs] = kInf;
-            if (hs * kS2Threads + w * 64 >= NH) continue;  // wave-uniform
-            const uint32_t x = hs * kS2Threads + t;
-            const bool ok = x < NH;
-            if (ok) {
-                const float bb = EHc[hh[hs]] + hv[hs];
-                const float vm = vread(hc[hs]);
-                HP[x] = make_float2(bb, vm);
-                cv[hs] = bb + vm;
-            }
-            if (uni & (1u << hs)) {
-                const float r = wave_min63(cv[hs]);
-                if (lane == 63) lds_min_u32(cmin + par * H + hh[hs], okey(r));
-            } else if (ok) {
-                lds_min_u32(cmin + par * H + hh[hs], okey(cv[hs]));
-            }
+        for (uint32_t h = t; h < H; h += kS2Threads) {
+            hacc[h] = okey(kInf);
+            cmin[(par ^ 1u) * H1 + h] = okey(kInf);
+            ccnt[(par ^ 1u) * H2 + h] = 0;
         }
-        __syncthreads();
-        // ---- phase 1b: candidates; next chunk's heavy E; resets for the next chunk
-#pragma unroll
-        for (int hs = 0; hs < NHS; ++hs) {
-            if (hs * kS2Threads + w * 64 >= NH) continue;
-            const uint32_t x = hs * kS2Threads + t;
-            const bool ok = x < NH;
-            const uint32_t h = ok ? hh[hs] : 0;
-            const bool cand = ok && cv[hs] <= theta_of(okey_val(cmin[par * H + h]), amax[h], prune);
-            if (uni & (1u << hs)) {
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
-                if (bal) {
-                    uint32_t base = 0;
-                    if (lane == 0)
-                        base = __hip_atomic_fetch_add(ccnt + par * H + h, (uint32_t)__builtin_popcountll(bal),
-                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    if (cand) CL[hoff[h] + base + below] = (uint16_t)x;
-                }
-            } else if (cand) {
-                const uint32_t pos = __hip_atomic_fetch_add(ccnt + par * H + h, 1u, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
-                CL[hoff[h] + pos] = (uint16_t)x;
-            }
-        }
-        if (t < H) {
-            hacc[t] = okey(kInf);
-            cmin[(par ^ 1u) * H + t] = okey(kInf);
-            ccnt[(par ^ 1u) * H + t] = 0;
-            if (more) {
-                EH[(par ^ 1u) * 2 * H + t] = hn1;
-                EH[(par ^ 1u) * 2 * H + H + t] = hn2;
-            }
-        }
-        __syncthreads();
+        S2_T(2);
+        lds_barrier();
+        S2_T(3);
         // ---- phase 2: the chunk's products applied to v
 #pragma unroll
         for (int s = 0; s < R; ++s) {
+            if (s * kS2Threads + w * 64 >= n) continue;
             const uint32_t r = s * kS2Threads + t;
-            if (r < n) {
-                float acc = kInf;
-#pragma unroll
-                for (int k = 0; k < KL; ++k) {
-                    const uint32_t cc = lc[s][k];
-                    if (cc != kNone) acc = fminf(acc, inner(cc, e2[s] + lv[s][k], par));
-                }
-                vl[r] = acc;  // heavy rows' entries are unused (their scores live in hacc)
-            }
-        }
-#pragma unroll
-        for (int hs = 0; hs < NHS; ++hs) {
-            if (hs * kS2Threads + w * 64 >= NH) continue;
-            const uint32_t x = hs * kS2Threads + t;
-            const bool ok = x < NH;
             float acc = kInf;
-            if (ok) acc = inner(hc[hs], EHc[H + hh[hs]] + hv[hs], par);
-            if (uni & (1u << hs)) {
-                const float r = wave_min63(acc);
-                if (lane == 63) lds_min_u32(hacc + hh[hs], okey(r));
-            } else if (ok) {
-                lds_min_u32(hacc + hh[hs], okey(acc));
+#pragma unroll
+            for (int k = 0; k < KL; ++k) acc = fminf(acc, apply(lb[s][k], e2[s] + lv[s][k], ccp));
+            if (r < n) vl[r] = acc;  // heavy rows' entries stay unused (their scores live in hacc)
+        }
+        if (hwave) {
+            const float eh2 = EHc[H1 + hr];
+            float part = kInf;
+#pragma unroll
+            for (int hs = 0; hs < NHS; ++hs)
+                if ((uint32_t)hs < nhs) part = fminf(part, apply(hb[hs], eh2 + hv[hs], ccp));
+            if (huni) {
+                part = wave_min63(part);
+                if (lane == 63) lds_min_u32(hacc + hr, okey(part));
+            } else if (hr < H) {
+                lds_min_u32(hacc + hr, okey(part));
             }
         }
-        __syncthreads();
+        if (t < H && more) {  // the next chunk's heavy E (loaded at this chunk's start)
+            EH[(par ^ 1u) * 2 * H1 + t] = g1;
+            EH[(par ^ 1u) * 2 * H1 + H1 + t] = g2;
+        }
+        S2_T(4);
+        lds_barrier();
+        S2_T(5);
         if (more) {
 #pragma unroll
             for (int s = 0; s < R; ++s) {
@@ -327,6 +345,12 @@ __global__ __launch_bounds__(kS2Threads) void spec2_kernel(Spec2Model m, Spec2Ba
             }
         }
     }
+#ifdef SVH_SPEC2_DIAG
+    dg[6] = __builtin_amdgcn_s_memtime() - tloop;
+    dg[7] = nch;
+    if (m.stamps && lane == 0)
+        for (int k = 0; k < kSpec2Stamps; ++k) m.stamps[((size_t)q * 16 + w) * kSpec2Stamps + k] = dg[k];
+#endif
     for (uint32_t h = t; h < H; h += kS2Threads) vl[m.hrow[h]] = okey_val(hacc[h]);
     __syncthreads();
     for (uint32_t j = t; j < n; j += kS2Threads) vg[j] = vl[j];
@@ -337,37 +361,35 @@ const void* spec2_ptr() {
     return reinterpret_cast<const void*>(&spec2_kernel<R, KL, NHS>);
 }
 
+template <int R, int KL>
+const void* spec2_ptr_h(uint32_t NHS) {
+    return NHS == 4 ? spec2_ptr<R, KL, 4>() : NHS == 6 ? spec2_ptr<R, KL, 6>() : NHS == 8 ? spec2_ptr<R, KL, 8>() : nullptr;
+}
+
 const void* spec2_kernel_for(uint32_t R, uint32_t KL, uint32_t NHS) {
-    const uint32_t r = R <= 2 ? 2 : R <= 4 ? 4 : 0;
-    const uint32_t k = KL <= 2 ? 2 : KL <= 4 ? 4 : 0;
-    const uint32_t h = NHS <= 4 ? 4 : NHS <= 8 ? 8 : 0;
-    switch (r * 100 + k * 10 + h) {
-        case 224: return spec2_ptr<2, 2, 4>();
-        case 228: return spec2_ptr<2, 2, 8>();
-        case 244: return spec2_ptr<2, 4, 4>();
-        case 248: return spec2_ptr<2, 4, 8>();
-        case 424: return spec2_ptr<4, 2, 4>();
-        case 428: return spec2_ptr<4, 2, 8>();
-        case 444: return spec2_ptr<4, 4, 4>();
-        case 448: return spec2_ptr<4, 4, 8>();
+    switch (R * 10 + KL) {
+        case 22: return spec2_ptr_h<2, 2>(NHS);
+        case 24: return spec2_ptr_h<2, 4>(NHS);
+        case 32: return spec2_ptr_h<3, 2>(NHS);
+        case 34: return spec2_ptr_h<3, 4>(NHS);
+        case 42: return spec2_ptr_h<4, 2>(NHS);
+        case 44: return spec2_ptr_h<4, 4>(NHS);
         default: return nullptr;
     }
 }
 
 }  // namespace
 
-uint32_t spec2_round_r(uint32_t R) { return R <= 2 ? 2 : R <= 4 ? 4 : 0; }
+uint32_t spec2_round_r(uint32_t R) { return R <= 2 ? 2 : R <= 4 ? R : 0; }
 uint32_t spec2_round_kl(uint32_t KL) { return KL <= 2 ? 2 : KL <= 4 ? 4 : 0; }
-uint32_t spec2_round_nhs(uint32_t NHS) { return NHS <= 4 ? 4 : NHS <= 8 ? 8 : 0; }
+uint32_t spec2_round_nhs(uint32_t NHS) { return NHS <= 4 ? 4 : NHS <= 6 ? 6 : NHS <= 8 ? 8 : 0; }
 
 hipError_t launch_spec2(const Spec2Model& m, const Spec2Batch& b, hipStream_t stream) {
     const void* fn = spec2_kernel_for(m.R, m.KL, m.NHS);
-    if (!fn || m.H > kS2Threads || m.n > 65535 || m.NH > 65535 || m.R != spec2_round_r(m.R) ||
-        m.KL != spec2_round_kl(m.KL) || m.NHS != spec2_round_nhs(m.NHS) || m.n > m.R * kS2Threads ||
-        m.NH > m.NHS * kS2Threads)
+    if (!fn || m.H + 2 > kS2Threads || m.n > 65535 || m.nhs == 0 || m.nhs > m.NHS || m.n > m.R * kS2Threads)
         return hipErrorInvalidValue;
     if (b.nseq == 0) return hipSuccess;
-    const size_t lds = spec2_lds_layout(m.n, m.KL, m.NH, m.H).bytes;
+    const size_t lds = spec2_lds_layout(m.n, m.KL, m.NP, m.H).bytes;
     if (lds > kMaxLdsBytes) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

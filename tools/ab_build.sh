@@ -10,7 +10,9 @@ mkdir -p $D/obj
 # objects the flags do not change come from the tree's build (make then rebuilds only what differs:
 # pass REBUILD=all to build everything with the flags)
 if [ -z "$REBUILD" ] && [ -d build ]; then
-    for o in build/*.o; do case $o in build/pipe.o|build/pipe_tm1.o|build/pipe_tm1p.o) ;; *) cp -p $o $D/obj/ ;; esac; done
+    # AB_OBJS: the objects the flags change (default: the latency kernel's)
+    REB=" ${AB_OBJS:-pipe pipe_tm1 pipe_tm1p} "
+    for o in build/*.o; do b=$(basename $o .o); case "$REB" in *" $b "*) ;; *) cp -p $o $D/obj/ ;; esac; done
 fi
 make -j8 BUILD=$D/obj LIB=$D/libspec_viterbi_hip.so EXTRA_HIPFLAGS="$FLAGS" $D/libspec_viterbi_hip.so > $D/build.log 2>&1
 echo "built $D/libspec_viterbi_hip.so"
