@@ -60,6 +60,10 @@ constexpr uint32_t kR = kPipeRing;
 #define SVH_PIPE_GST 2
 #endif
 constexpr uint32_t kGpf = SVH_PIPE_GPF;
+// (Round 5, measured and not kept: four groups for a consumer whose producer sits on another XCD.
+// The cross-XCD rows, 2 of the headline's 50, end the launch 15-25 us after the XCD-local ones; with
+// four groups in flight their prefetches outran the producer and polled: 0.296-0.306 ms against
+// 0.250-0.254, profiles/r05_s8.)
 constexpr uint32_t kGst = SVH_PIPE_GST;
 static_assert(kGpf == 1 || kGpf == 2 || kGpf == 4, "granule prefetch depth");
 static_assert(kGst < 8, "granule store step");
@@ -443,7 +447,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             }
         };
         auto ring_put2 = [&](uint32_t t) {  // {light minimum of t-1, sink partial of t}
+#ifndef SVH_PIPE_NO_PRING  // ablation (timing only, wrong paths): the per-step LDS store's price
             *reinterpret_cast<float2*>(pring_w + (t & 31u) * kPRingStride + lane * 2) = make_float2(last_pm, CF.x);
+#endif
         };
         // fold rows tb .. tb+31 of the ring (tb % 32 == 0) and store observations t in [1, thi):
         // lane l reduces row l % 32 over the half-wave l / 32 (conflict-free: rows 528 B apart)
@@ -829,6 +835,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 
         // The sweep, with the boundary roles as compile-time constants (one code path per role).
         auto sweep = [&](auto srcc, auto dstc) {
+            constexpr uint32_t GPF = kGpf;  // granule groups in flight (SRC 2)
             constexpr int SRC = decltype(srcc)::value, DST = decltype(dstc)::value;
             // one observation outside the unrolled groups: per-observation waits
             auto single = [&](uint32_t t) {
@@ -891,10 +898,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 
             // body: 32 observations per iteration, four groups of 8
             if (t + 32 <= len) {
-                uint64_t gq[kGpf] = {};  // SRC 2: granule groups in flight
+                uint64_t gq[GPF] = {};  // SRC 2: granule groups in flight
                 if constexpr (SRC == 2) {
 #pragma unroll
-                    for (uint32_t j = 0; j < kGpf; ++j) g_prefetch64(gq[j], gin + ((t + 8 * j + (lane & 7u)) & (kGR - 1)));
+                    for (uint32_t j = 0; j < GPF; ++j) g_prefetch64(gq[j], gin + ((t + 8 * j + (lane & 7u)) & (kGR - 1)));
                 }
                 float gpend = 0.0f;    // DST 2: the previous group's boundary scores (lanes 0..7),
                 uint32_t gpend_t = 0;  // read back from the ring one group before they are stored
@@ -939,8 +946,8 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         float bv = kInf;  // lanes 0..7: the previous block's last scores of tg..tg+7
                         float gl[8];      // SVH_PIPE_RING8: this group's last-slot scores
                         if constexpr (SRC == 2) {
-                            wait_vmcnt<kGpf - 1>();  // gq[j]: kGpf - 1 later loads in flight
-                            uint64_t gv = gq[j % kGpf];
+                            wait_vmcnt<GPF - 1>();  // gq[j]: GPF - 1 later loads in flight
+                            uint64_t gv = gq[j % GPF];
                             while (!kNoWait && __builtin_amdgcn_ballot_w64((uint32_t)(gv >> 32) != gtag(ep, tg)) != 0) {
                                 if (dbg) ++dg[5];
                                 if (give_up()) break;
@@ -948,7 +955,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                 gv = g_ld64(gin + ((tg + (lane & 7u)) & (kGR - 1)));
                             }
                             bv = __builtin_bit_cast(float, (uint32_t)gv);
-                            g_prefetch64(gq[j % kGpf], gin + ((tg + 8 * kGpf + (lane & 7u)) & (kGR - 1)));
+                            g_prefetch64(gq[j % GPF], gin + ((tg + 8 * GPF + (lane & 7u)) & (kGR - 1)));
                         }
                         if constexpr (DST == 1) {
                             if constexpr (SVH_PIPE_LDSX) asm volatile("" : "+v"(nc_rd));

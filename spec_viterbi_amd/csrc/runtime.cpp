@@ -1000,11 +1000,15 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
         cu_count = (uint32_t)cus;
         if (pipe.plan.ok) pipe.view.cus = cu_count;  // latency plan: the XCD-class mapping's residency test
         if (pipe.plan.ok) {
-            // AUTO: the latency plan while the batch gives every CU at most one of its workgroups
-            // (one wave per SIMD); wider batches run the wide pipelined plan (measured: DESIGN.md
-            // 5c), or the chain kernel where the model has none; SVH_PIPE_MAX_NSEQ overrides
-            pipe_max_nseq = std::max<uint32_t>(1, cu_count / pipe.plan.G);
-            if (!pipe_wide.plan.ok) pipe_max_nseq = std::max<uint32_t>(1, 2 * cu_count / pipe.plan.G);
+            // AUTO: scores-only batches take the latency plan while they give every CU at most two
+            // of its workgroups (two waves per SIMD: the scores kernel's 232 VGPRs fit twice;
+            // 2405 x 100 sequences 0.323 ms against 0.427 on the wide plan, 150 sequences 0.574
+            // against 0.429, profiles/r05_s10); decoded-path batches while they give every CU at most
+            // one (the path kernel's 290 registers fit once); wider batches run the wide pipelined plan
+            // (DESIGN.md 5c), or the chain kernel where the model has none; SVH_PIPE_MAX_NSEQ
+            // overrides the scores-only bound
+            pipe_max_nseq = std::max<uint32_t>(1, 2 * cu_count / pipe.plan.G);
+            pipe_max_nseq_paths = std::max<uint32_t>(1, cu_count / pipe.plan.G);
             if (const char* e = std::getenv("SVH_PIPE_MAX_NSEQ")) pipe_max_nseq = (uint32_t)std::atoi(e);
         }
         if (pipe_wide.plan.ok) {
@@ -1100,8 +1104,8 @@ const DevicePipePlan* Model::pipe_paths_for(uint32_t nseq) const {
     if (kernel_pref == SVH_KERNEL_PIPE) return lat ? &pipe : nullptr;
     if (kernel_pref == SVH_KERNEL_PIPE_WIDE) return wid ? &pipe_wide : nullptr;
     if (kernel_pref != SVH_KERNEL_AUTO) return nullptr;
-    if (lat && nseq <= pipe_max_nseq) return &pipe;
-    if (wid && nseq >= pipew_min_nseq) return &pipe_wide;
+    if (lat && nseq <= pipe_max_nseq_paths) return &pipe;
+    if (wid && nseq > pipe_max_nseq_paths) return &pipe_wide;
     return nullptr;
 }
 
@@ -2108,7 +2112,11 @@ void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) co
             hip_check(hipStreamSynchronize(s), "stamps");
             ppl->report_stamps(b.nseq);
         }
-        // rows whose speculation failed run again on the serial chain kernel (the others exit)
+        // rows whose speculation failed run again on the serial chain kernel (the others exit);
+        // SVH_PIPE_SKIP_FALLBACK=1: diagnostics only (timing without the second launch; results of
+        // flagged rows would be wrong)
+        static const bool skip_fb = std::getenv("SVH_PIPE_SKIP_FALLBACK") && std::atoi(std::getenv("SVH_PIPE_SKIP_FALLBACK"));
+        if (skip_fb) return;
         FusedBatch fb = b;
         fb.run_mask = b.pipe->viol;
         fb.pipe = nullptr;

@@ -223,7 +223,8 @@ struct Model {
                                      // 4 waves (more workgroups per CU), scores only
     uint32_t cu_count = 0;
     DevicePipePlan pipe;             // pipelined chain plan (latency path for small batches)
-    uint32_t pipe_max_nseq = 0;      // AUTO: pipelined plan for batches of at most this many rows
+    uint32_t pipe_max_nseq = 0;      // AUTO: pipelined plan for scores-only batches of at most this many rows
+    uint32_t pipe_max_nseq_paths = 0;  // ... for decoded-path batches
     DevicePipePlan pipe_wide;        // wide pipelined plan (throughput path for batches that fill the chip)
     uint32_t pipew_min_nseq = 0;     // AUTO: wide pipelined plan for batches of at least this many rows
     DevicePlan fast_plan;            // fastest fused plan (may use uniform heavy rows)

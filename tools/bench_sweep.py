@@ -10,8 +10,11 @@ Per cell:
   ms_setup    non-spec only: the same plus svh_model_create inside every run, as the reference
               times run_Viterbi with its per-call model build (bench_Viterbi.h:53-56)
   prep_ms     spec only: spec_with (svh_spec_build), timed apart as bench_Viterbi_spec.h:69-71
-  check       the first sequence against the CPU oracle: "bit-exact" (scores bit-identical), or
-              for level 2 on models with n > 600 (the oracle's products would take minutes)
+  check       "digests": every sequence bit-exact against the committed oracle digests where they
+              exist (tests/golden/scope_digests.json: every model x emit_3_3500_20, non-spec and
+              level 2; score_digests.json: 2405 x emit_50 / covid-19, 100 x emit_3, 2405 x emit_50
+              level 2); otherwise the first sequence against the CPU oracle, "bit-exact", or for
+              level 2 on models with n > 600 (the oracle's products would take minutes)
               "almost_equal-L0" (every sequence within HMM::almost_equal of the non-spec scores)
 
     python3 tools/bench_sweep.py [--models 100.chmm,2405.chmm] [--levels 0,1,2] [--out FILE]
@@ -20,6 +23,7 @@ from __future__ import annotations
 
 import argparse
 import glob
+import hashlib
 import json
 import os
 import statistics
@@ -37,6 +41,21 @@ from tests.helpers import bit_equal  # noqa: E402
 
 DATASETS = ["emit_3_3500_20.ess", "emit_3_7000_20.ess", "covid-19.ess", "emit_50_3500_20.ess"]
 RUNS = 10
+
+
+def digest_rows(model: str, dataset: str, level: int):
+    """SHA-256 digests of the oracle's rows for this cell (level 0/1 share the non-spec rows), or None."""
+    g = os.path.join(ROOT, "tests", "golden")
+    with open(os.path.join(g, "scope_digests.json")) as f:
+        scope = json.load(f)
+    with open(os.path.join(g, "score_digests.json")) as f:
+        sd = json.load(f)
+    if dataset == scope["ess"] and model in scope["models"]:
+        key = "scores_sha256" if level <= 1 else "spec2_sha256" if level == 2 else None
+        if key:
+            return [r[key] for r in scope["models"][model]]
+    k = f"{model} x {dataset}" + ("" if level <= 1 else f" level {level}")
+    return [r["scores_sha256"] for r in sd[k]] if k in sd else None
 
 
 def timed(fn, runs=RUNS):
@@ -83,7 +102,13 @@ def main():
                         m.close()
                     ms_setup = timed(with_setup)
                 scores, _ = model.viterbi(seqs, level=lv)
-                if lv <= 1:
+                ref = digest_rows(name, dname, lv)
+                if ref is not None:
+                    ok = len(ref) == len(seqs) and all(
+                        hashlib.sha256(np.ascontiguousarray(scores[q], np.float32).tobytes()).hexdigest() == ref[q]
+                        for q in range(len(seqs)))
+                    check = "digests" if ok else "MISMATCH"
+                elif lv <= 1:
                     ok = bit_equal(scores[0], oracle.viterbi(hmm, seqs[0]))
                     check = "bit-exact" if ok else "MISMATCH"
                 elif n <= 600:

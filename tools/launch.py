@@ -52,8 +52,9 @@ def main():
         times.append(batch.elapsed_ms())
     scores, _ = batch.read()
     ok = None
-    # (diagnostic ablations, SVH_*_DEBUG, give wrong results by design: not checked)
-    diag = any(os.environ.get(k) for k in ("SVH_PIPE_DEBUG", "SVH_BAND_DEBUG"))
+    # (diagnostic ablations, SVH_*_DEBUG or SVH_LAUNCH_NOCHECK=1 for ablation builds, give wrong
+    # results by design: not checked)
+    diag = any(os.environ.get(k) for k in ("SVH_PIPE_DEBUG", "SVH_BAND_DEBUG", "SVH_LAUNCH_NOCHECK"))
     if a.model == "2405.chmm" and a.ess == "emit_50_3500_20.ess" and a.level <= 2 and not diag:
         import hashlib
 
