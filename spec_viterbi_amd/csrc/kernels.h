@@ -261,13 +261,19 @@ inline uint64_t pipe_mask_words(uint64_t len, uint32_t nblk, uint32_t sm) {
     return len > 1 ? (len - 1 + 31) / 32 * (uint64_t)nblk * sm * 64 : 0;
 }
 // heavy partials per block and observation: 2 (latency plan: one per half-wave), 1 (wide plan)
-__host__ __device__ inline uint32_t pipe_prec_parts(bool wide) { return wide ? 1u : 2u; }
+// heavy partials per block and observation: 1 on both plans (the latency plan folded its ring per
+// half-wave into 2 until round 4)
+__host__ __device__ inline uint32_t pipe_prec_parts(bool wide) { (void)wide; return 1u; }
 inline uint64_t pipe_prec_count(uint64_t len, uint32_t nblk, uint32_t parts) { return (uint64_t)nblk * parts * len; }
 inline uint64_t pipe_ckpt_floats(uint64_t len, uint32_t P) { return len ? ((len - 1) / kCkptEvery + 1) * (uint64_t)P : 0; }
 inline uint64_t pipe_fck_floats(uint64_t len) { return len ? (len - 1) / 32 + 1 : 0; }
 // LDS of the decoded-path variant beyond pipe_lds_bytes: a ring of 32 rows {pm, c} per wave
 constexpr uint32_t kPRingStride = 132;  // floats per row: 64 lanes x 2 + 4 padding (bank spread)
-inline size_t pipe_path_lds_bytes(uint32_t W) { return (size_t)W * 32 * kPRingStride * 4; }
+// Latency plan (pipe_kernel.h PATHS): per wave 8 quads (4 observations each) of 64 lanes x 8 floats,
+// lanes 32..63 of a quad 128 bytes after lanes 0..31 and quads kPQuadStride floats apart, so the
+// transposed fold (lane = observation, reading 32 lanes' pairs) hits every bank pair at most twice.
+constexpr uint32_t kPQuadStride = 584;  // floats: 64 x 8 + 32 (half gap) + 40 (bank spread)
+inline size_t pipe_path_lds_bytes(uint32_t W) { return (size_t)W * 8 * kPQuadStride * 4; }
 // Wide pipelined plan (pipe_wide.hip): one block of 64*SM positions per workgroup, W sequences
 // (one per wave), the block's table [nblk][S][NC][64] float4 in LDS (PipeModel.tab; G = nblk);
 // NC = SM/2 (eb|ea) chunks + {A_S A_F X_SS X_FF} [+ {X_SF 0 0 0} when sx], constants per lane.

@@ -261,7 +261,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     float* ctab = reinterpret_cast<float*>(cnt + 16);                   // [S][8]
     float* red = ctab + m.S * 8;                                        // [W][4]
     uint32_t* tick = reinterpret_cast<uint32_t*>(red + W * 4);
-    // PATHS: [W][32][kPRingStride] rows {pm, c} per lane, 16-byte aligned after the rest
+    // PATHS: [W][8 quads][kPQuadStride] {pm, c} of 4 observations per lane, 16-byte aligned after the rest
     float* pring = lds + (pipe_lds_bytes(W, m.S) + 15) / 16 * 4;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -426,7 +426,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         }
 
         // ---- decoded paths: outputs and the per-slot tie masks
-        float* const pring_w = pring + w * 32 * kPRingStride;
+        float* const pring_w = pring + w * 8 * kPQuadStride;
+        // lane l's 32 bytes in quad q (observations 4q..4q+3 of the cycle of 32)
+        float* const pring_l = pring_w + lane * 8 + (lane >= 32 ? 32 : 0);
+        float pst[8];  // this quad's {pm, c} pairs, written by two ds_write_b128 at its last step
         uint32_t* const cmq = PATHS ? b.cmask + b.cmask_off[q] : nullptr;
         float* const ckq = PATHS ? b.ckpt + b.ckpt_off[q] : nullptr;
         float2* const precq = PATHS ? b.prec + b.prec_off[q] : nullptr;
@@ -446,32 +449,48 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 for (int s = 0; s < SM; ++s) d[s] = v[s];
             }
         };
-        auto ring_put2 = [&](uint32_t t) {  // {light minimum of t-1, sink partial of t}
-#ifndef SVH_PIPE_NO_PRING  // ablation (timing only, wrong paths): the per-step LDS store's price
-            *reinterpret_cast<float2*>(pring_w + (t & 31u) * kPRingStride + lane * 2) = make_float2(last_pm, CF.x);
-#endif
+        // {light minimum of t-1, sink partial of t}: kept in registers for the 4 observations of a
+        // quad and written by its last step as two ds_write_b128 (one LDS store per step cost 40 us
+        // of the 388 us path kernel on the headline, profiles/r05_s11); single observations (head,
+        // tail) write their own pair
+        auto ring_put2 = [&](auto rc) {  // rc: the observation's place in its quad (compile time)
+            constexpr uint32_t r = decltype(rc)::value;
+            pst[2 * r] = last_pm;
+            pst[2 * r + 1] = CF.x;
         };
-        // fold rows tb .. tb+31 of the ring (tb % 32 == 0) and store observations t in [1, thi):
-        // lane l reduces row l % 32 over the half-wave l / 32 (conflict-free: rows 528 B apart)
+        auto ring_flush = [&](uint32_t t) {  // t % 4 == 3: the quad of t is complete
+            float4* d = reinterpret_cast<float4*>(pring_l + ((t >> 2) & 7u) * kPQuadStride);
+            d[0] = make_float4(pst[0], pst[1], pst[2], pst[3]);
+            d[1] = make_float4(pst[4], pst[5], pst[6], pst[7]);
+        };
+        auto ring_put1 = [&](uint32_t t) {
+            *reinterpret_cast<float2*>(pring_l + ((t >> 2) & 7u) * kPQuadStride + (t & 3u) * 2) = make_float2(last_pm, CF.x);
+        };
+        // fold observations tb .. tb+31 (tb % 32 == 0) and store those in [1, thi): lane l takes
+        // observation o = l % 32 over the half-wave of source lanes l / 32, then the two halves
+        // combine (one swizzle) and lanes 0..31 store one record per observation
         auto reduce_ring = [&](uint32_t tb, uint32_t thi) {
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
-            const uint32_t R = lane & 31u, H = lane >> 5;
-            const float4* rp = reinterpret_cast<const float4*>(pring_w + R * kPRingStride + H * 64);
+            const uint32_t o = lane & 31u, H = lane >> 5;
+            const float* rp = pring_w + (o >> 2) * kPQuadStride + H * (32 * 8 + 32) + (o & 3u) * 2;
             float mm = kInf, cc = kInf;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const float4 e = rp[i];
-                mm = fminf(mm, fminf(e.x, e.z));
-                cc = fminf(cc, fminf(e.y, e.w));
+            for (int L = 0; L < 32; ++L) {
+                const float2 e = *reinterpret_cast<const float2*>(rp + L * 8);
+                mm = fminf(mm, e.x);
+                cc = fminf(cc, e.y);
             }
-            const uint32_t tt = tb + R;
-            if (tt >= 1 && tt < thi) precq[((size_t)blk * 2 + H) * len + tt] = make_float2(mm, cc);
+            mm = fminf(mm, __shfl_xor(mm, 32));
+            cc = fminf(cc, __shfl_xor(cc, 32));
+            const uint32_t tt = tb + o;
+            if (H == 0 && tt >= 1 && tt < thi) precq[(size_t)blk * len + tt] = make_float2(mm, cc);
         };
         // after the step of observation t (compile-time positions in the unrolled body)
-        auto paths_after = [&](uint32_t t, auto maskc, auto ckc, auto redc) {
+        auto paths_after = [&](uint32_t t, auto maskc, auto ckc, auto redc, auto rc) {
             if constexpr (PATHS) {
-                ring_put2(t);
+                ring_put2(rc);
+                if constexpr (decltype(rc)::value == 3) ring_flush(t);
                 if constexpr (decltype(maskc)::value) {
                     if (t >= 32) store_masks((t >> 5) - 1, 32);
                     if (blk == 0 && lane == 0) fckq[t >> 5] = CF.y;
@@ -482,7 +501,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         };
         auto paths_after_rt = [&](uint32_t t) {  // runtime positions (head / tail)
             if constexpr (PATHS) {
-                ring_put2(t);
+                ring_put1(t);
                 if ((t & 31u) == 0) {
                     if (t >= 32) store_masks((t >> 5) - 1, 32);
                     if (blk == 0 && lane == 0) fckq[t >> 5] = CF.y;
@@ -989,7 +1008,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             }
                             paths_after(tg + k, std::bool_constant<j == 0 && k == 0>{},
                                         std::bool_constant<k == 0 && (j == 0 || j == 2)>{},
-                                        std::bool_constant<j == 3 && k == 7>{});
+                                        std::bool_constant<j == 3 && k == 7>{}, std::integral_constant<uint32_t, k & 3u>{});
                             if constexpr (k == 4) {  // the counts checked at the end of the group
                                 asm volatile("" ::: "memory");
                                 if constexpr (SRC == 1) pc_rd = lds_ld32(cnt_w - 1);

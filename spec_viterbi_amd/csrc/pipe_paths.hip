@@ -7,8 +7,8 @@
 // position and observation, whether F's term was taken (mask words); the heavy rows' inputs of an
 // observation -- F's and S's scores and the light minimum mu -- are rebuilt where the walk needs
 // them from the kernel's per-block partials (RecSrc):
-//       mu(r) = min over blocks and half-waves of prec[.][.][r+1].x   (exact: min is exact)
-//       C(r)  = min over blocks and half-waves of prec[.][.][r].y, C(0) = fl(E_S(o_0) + start_S)
+//       mu(r) = min over blocks of prec[.][r+1].x   (exact: min is exact)
+//       C(r)  = min over blocks of prec[.][r].y, C(0) = fl(E_S(o_0) + start_S)
 //       F(r)  = F(32k) from fck, advanced by F = fl(X_FF(o_i) + F) (the kernel's speculated F,
 //               exact for every row the kernel did not flag)
 // The walk (one wave per sequence) is chain_paths.hip's chain_traceback_kernel -- speculative
@@ -33,7 +33,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // The heavy rows' inputs of record row r (observation r+1), rebuilt on demand from the kernel's
-// per-block partials (prec[u][t] = {mu_u(t-1), C_u(t)}, u over blocks x half-waves) and F's
+// per-block partials (prec[u][t] = {mu_u(t-1), C_u(t)}, u over blocks) and F's
 // 32-observation checkpoints: min is exact, and F is re-advanced with the kernel's own
 // fl(X_FF(o) + F).
 struct RecSrc {
