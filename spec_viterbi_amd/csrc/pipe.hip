@@ -63,12 +63,15 @@ hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratc
     FusedBatch bb = b;
     PipeScratch xx = x;
     void* args[] = {&mm, &bb, &xx};
-    const uint64_t grid = (uint64_t)b.nseq * m.G;
+    uint64_t grid = (uint64_t)b.nseq * m.G;
     // XCD-class mapping of rows to workgroups when the launch fits the chip at one workgroup per CU
     // (pipe_kernel.h: per-class tickets in start order, deadlock-free whatever else holds CUs; the
     // size condition is about speed only); SVH_PIPE_XMAP=0 keeps the single ticket counter (A/B)
     static const bool xmap_env = !(std::getenv("SVH_PIPE_XMAP") && std::atoi(std::getenv("SVH_PIPE_XMAP")) == 0);
-    xx.xmap = xmap_env && m.cus && grid <= m.cus ? 1u : 0u;
+    // (the grid padded to a multiple of 8, equal classes: pipe_kernel.h; padding slots exit at once)
+    const uint64_t padded = (grid + 7) & ~7ull;
+    xx.xmap = xmap_env && m.cus && padded <= m.cus ? 1u : 0u;
+    if (xx.xmap) grid = padded;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const size_t lds = paths ? (pipe_lds_bytes(m.W, m.S) + 15) / 16 * 16 + pipe_path_lds_bytes(m.W)
                              : pipe_lds_bytes(m.W, m.S);

@@ -109,6 +109,27 @@ __device__ __forceinline__ void wait_vmcnt() {
 #define SVH_PIPE_XL 1
 #endif
 
+// The next group's boundary vector (SRC 1) read at step 4, right after the producer's count it is
+// validated against (A/B knob SVH_PIPE_EARLYV): LDS executes one CU's instructions in order and the
+// producer wrote its ring before its count, so a count that covers the group guarantees the vector
+// read issued after it sees the group; otherwise the slow path waits and reads it again.  At the
+// group's end (0) the read's latency sat in front of the next group's second step.
+#ifndef SVH_PIPE_EARLYV
+#define SVH_PIPE_EARLYV 1
+#endif
+
+// Exchange helpers (A/B knob SVH_PIPE_XHELP, workgroups of three waves or more): the vector-memory
+// counter retires a wave's loads and stores in issue order, so a wave that both stores to another
+// XCD (write-through, acknowledged late) and waits for a load waits for those stores too.  The
+// granule reader (wave 0) published its progress word and the granule writer (wave W - 1) loaded
+// its consumer's, so on the rows whose hops cross XCDs both waited on remote stores every 32
+// observations.  With the helpers wave 1, which has no other global traffic, publishes the progress
+// (its own, never ahead of wave 0's) and wave W - 2 loads the consumer's word once per 32
+// observations into an LDS slot that wave W - 1 reads: wave 0 only loads and wave W - 1 only stores.
+#ifndef SVH_PIPE_XHELP
+#define SVH_PIPE_XHELP 1
+#endif
+
 // Diagnostic ablation (-DSVH_PIPE_NOWAIT, timing only, wrong results): every exchange operation
 // runs, but no wait on a neighbour does (counts, flow control, granule tags and progress words are
 // taken as ready): the rate of a wave when no neighbour ever holds it up.
@@ -251,6 +272,16 @@ struct ChainIn {
     float b;
 };
 
+// The last workgroup of a launch to finish (every one has taken its ticket and read the epoch):
+// tickets and the finish count back to 0, the epoch advanced (ctr[2] + 1 is this launch's).
+__device__ __forceinline__ void pipe_reset_counters(const PipeScratch& x) {
+    const uint32_t ep = __hip_atomic_load(x.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __hip_atomic_store(x.ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(x.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t c = kCtrClass; c <= kCtrLeft; ++c) __hip_atomic_store(x.ctr + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(x.ctr + 2, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int SM, int W, bool SX, int PATHS, int TM>
 __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     static_assert(TM == 0 || SM == 2, "pair tables: two slots per lane");
@@ -270,31 +301,26 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     // (row, workgroup) of this workgroup, from a ticket taken in start order, so a consumer's
     // producer has always started before it (no deadlock when the grid exceeds residency or other
     // launches hold CUs).  Default: one ticket counter, rows in ticket order.  x.xmap (the runtime
-    // sets it when the launch fits the chip at one workgroup per CU): per-class tickets, so that a
-    // row's G workgroups share an XCD class (blocks b and b + 8 share an XCD under the observed
-    // round-robin placement; speed only -- the hand-offs check the real XCC ids, SVH_PIPE_XL).
-    // Class r = b % 8 holds n_r blocks and takes f_r = n_r / G rows whole: its k-th ticket (k <
-    // f_r G) is member k % G of its (k / G)-th row.  Its remaining tickets take a second ticket from
-    // one shared leftover counter, which forms the remaining rows in that counter's order.  Within a
-    // class and within the leftover rows the members of a row are numbered in start order, as
-    // with the single counter.
+    // sets it when the launch fits the chip at one workgroup per CU, the grid padded to a multiple
+    // of 8): per-class tickets, so that a row's G workgroups share an XCD class (blocks b and b + 8
+    // share an XCD under the observed round-robin placement; speed only -- the hand-offs check the
+    // real XCC ids, SVH_PIPE_XL).  Every class r = b % 8 holds n = N / 8 blocks and takes f = n / G
+    // rows whole: its k-th ticket (k < f G) is member k % G of row r f + k / G, members numbered in
+    // start order.  The n - f G spare tickets of the classes, in class order, form the remaining
+    // rows (slot u = r (n - f G) + k - f G is member u % G of row 8 f + u / G), so a remaining row
+    // spans at most three classes with two changes (its granule hops cross XCDs only there: each
+    // such hop slowed the rows that took the leftover tickets in start order by a few us); slots and
+    // rows past the batch are dummies that only count themselves finished.
     if (tid == 0) {
         uint32_t t;
         if (x.xmap) {
-            const uint32_t N = gridDim.x, r = blockIdx.x & 7u;
-            uint32_t pf = 0, fr = 0, F = 0;
-            for (uint32_t rr = 0; rr < 8; ++rr) {
-                const uint32_t n = N > rr ? (N - rr + 7) / 8 : 0, f = n / G;
-                F += f;
-                if (rr < r) pf += f;
-                if (rr == r) fr = f;
-            }
+            const uint32_t n = gridDim.x >> 3, r = blockIdx.x & 7u, f = n / G, sp = n - f * G;
             const uint32_t k = __hip_atomic_fetch_add(x.ctr + kCtrClass + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (k < fr * G) {
-                t = (pf + k / G) * G + k % G;
+            if (k < f * G) {
+                t = (r * f + k / G) * G + k % G;
             } else {
-                const uint32_t u = __hip_atomic_fetch_add(x.ctr + kCtrLeft, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                t = (F + u / G) * G + u % G;
+                const uint32_t u = r * sp + (k - f * G);
+                t = (8 * f + u / G) * G + u % G;
             }
         } else {
             t = __hip_atomic_fetch_add(x.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -306,6 +332,13 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     __syncthreads();
     const uint32_t id = (uint32_t)uniform((int)*tick);
     const uint32_t q = id / G, g = id - q * G;
+    if (q >= b.nseq) {  // x.xmap: a padding slot of the grid (no row); counts itself finished
+        if (tid == 0) {
+            const uint32_t f = __hip_atomic_fetch_add(x.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (f == gridDim.x - 1) pipe_reset_counters(x);
+        }
+        return;
+    }
     const uint32_t ep = (uint32_t)uniform((int)__hip_atomic_load(x.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
 #if SVH_PIPE_XL
     const uint32_t my_xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xFu;  // hwreg(HW_REG_XCC_ID, 0, 4)
@@ -759,6 +792,14 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         uint64_t* const gout = x.gran + ((size_t)q * (G - 1) + g) * kGR;       // dst == 2
         uint64_t* const cons_in = reinterpret_cast<uint64_t*>(x.cons) + (size_t)q * G + g;      // src == 2 publishes
         const uint64_t* const cons_out = reinterpret_cast<const uint64_t*>(x.cons) + (size_t)q * G + g + 1;  // dst == 2 reads
+        // SVH_PIPE_XHELP: wave 1 publishes this workgroup's progress (helped: wave 0 does not), wave
+        // W - 2 forwards the consumer's word to wave W - 1 through consf (cnt[14..15])
+        constexpr bool kXh = SVH_PIPE_XHELP && W >= 3;
+        static_assert(W <= 14, "cnt[14..15] holds the forwarded progress word");
+        uint64_t* const consf = reinterpret_cast<uint64_t*>(cnt + 14);
+        const bool helped = kXh && g > 0 && g * W + 1 < m.nblk;
+        const bool hpub = helped && w == 1;
+        const bool hrd = kXh && w == (uint32_t)W - 2 && (g + 1) * W < m.nblk;
         float bprev = kInf;  // boundary score of observation t-1 for the next step (uniform)
 
         auto give_up = [&]() -> bool { return ++spins > kSpinLimit; };
@@ -879,28 +920,33 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 }
                 asm volatile("" ::: "memory");
                 put_cnt(t + 1);
-                if constexpr (SRC == 2) {
+                if ((SRC == 2 && !helped) || (SRC == 1 && hpub)) {
                     if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | (t + 1));
                 }
             };
 
             if constexpr (SVH_PIPE_XL && DST == 2) gran_plain = xcc_local(g + 1);
             if constexpr (SVH_PIPE_XL && SRC == 2) cons_plain = xcc_local(g - 1);
+            if constexpr (SVH_PIPE_XL && SRC == 1 && kXh) {
+                if (hpub) cons_plain = xcc_local(g - 1);
+            }
             // publish the state at first-1 and fetch the boundary of first-1
             ring_put(first - 1, v[SM - 1]);
             if constexpr (DST == 2) put_gran1(first - 1, readlane_f(v[SM - 1], 63));
             asm volatile("" ::: "memory");
             put_cnt(first);
+            // initial progress (observations < first are done), published before the first wait:
+            // a row that starts mid-sequence at a multiple of 64 would otherwise leave its producer's
+            // first flow-control wait on a stale word while wave 0 waits for that producer's
+            // granules (the poll awaits observations up to first+6)
+            if ((SRC == 2 && !helped) || (SRC == 1 && hpub)) {
+                if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | first);
+            }
             if constexpr (SRC == 1) {
                 wait_prev(first);
                 asm volatile("" ::: "memory");
                 bprev = readlane_f(ring_prev[ring_idx((first - 1 - tb) & (kR - 1), 63)], 0);
             } else if constexpr (SRC == 2) {
-                // initial progress (observations < first are done), published before the first
-                // poll: a row that starts mid-sequence at a multiple of 64 would otherwise leave its
-                // producer's first flow-control wait on a stale word while this wave waits for that
-                // producer's granules (the poll awaits observations up to first+6)
-                if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | first);
                 bprev = gran_single(first - 1);
             }
 
@@ -926,6 +972,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 uint32_t gpend_t = 0;  // read back from the ring one group before they are stored
                 uint64_t cons_v = 0;   // DST 2: prefetched progress word of the consumer
                 if constexpr (DST == 2) cons_v = g_ld64(cons_out);
+                uint64_t cons_h = 0;   // SVH_PIPE_XHELP, wave W - 2: the word loaded for consf
+                if constexpr (DST == 1 && kXh) {
+                    if (hrd) cons_h = g_ld64(cons_out);
+                }
                 // counts of the neighbouring waves, read two observations before the end of a group
                 uint32_t pc_rd = 0, nc_rd = 0;
                 if constexpr (DST == 1) nc_rd = lds_ld32(cnt_w + 1);
@@ -936,6 +986,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 // SRC 1: the next group's vector, loaded at the end of every group (stale unless
                 // next_ok) into this one loop-carried register, re-loaded there when it was stale
                 float bv_next = kInf;
+                float bv_spec = kInf;  // SVH_PIPE_EARLYV: the next group's vector read at step 4
                 bool next_ok = false;
                 if constexpr (SRC == 1) bv_next = ring_prev[ring_idx(lane & 7u, 63)];  // group at t (u % 32 == 0)
                 while (t + 32 <= len) {
@@ -957,7 +1008,14 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                     const uint64_t sw3 = (uint64_t)readlane_u(cw.z, ln + 1) | ((uint64_t)readlane_u(cw.w, ln + 1) << 32);
                     if constexpr (DST == 2) {  // granule ring flow control, once per 32 observations
                         if (!cons_ok(uni64(cons_v), (int)t + 32 - (int)kGR + 8)) wait_cons((int)t + 32 - (int)kGR + 8);
-                        cons_v = g_ld64(cons_out);
+                        if constexpr (kXh) cons_v = __hip_atomic_load(consf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        else cons_v = g_ld64(cons_out);
+                    }
+                    if constexpr (DST == 1 && kXh) {  // forward last iteration's load, issue the next
+                        if (hrd) {
+                            if (lane == 0) __hip_atomic_store(consf, cons_h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            cons_h = g_ld64(cons_out);
+                        }
                     }
                     auto group = [&](auto jc, uint64_t sw) {
                         constexpr uint32_t j = decltype(jc)::value;
@@ -1013,6 +1071,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                 asm volatile("" ::: "memory");
                                 if constexpr (SRC == 1) pc_rd = lds_ld32(cnt_w - 1);
                                 if constexpr (DST == 1) nc_rd = lds_ld32(cnt_w + 1);
+                                if constexpr (SRC == 1 && SVH_PIPE_EARLYV) {  // after the count it is checked against
+                                    asm volatile("" ::: "memory");
+                                    bv_spec = ring_prev[ring_idx(((8 * j + 8) & (kR - 1)) + (lane & 7u), 63)];
+                                }
                                 // SVH_PIPE_LDSX: issued here, not where the scheduler would sink them (the
                                 // group's end, right before their use)
                                 if constexpr (SVH_PIPE_LDSX) __builtin_amdgcn_sched_barrier(0);
@@ -1040,7 +1102,8 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             if constexpr (SVH_PIPE_LDSX) asm volatile("" : "+v"(pc_rd));
                             next_ok = kNoWait || (uint32_t)uniform((int)pc_rd) >= tg + 16;
                             asm volatile("" ::: "memory");
-                            bv_next = ring_prev[ring_idx(((8 * j + 8) & (kR - 1)) + (lane & 7u), 63)];
+                            if constexpr (SVH_PIPE_EARLYV) bv_next = bv_spec;
+                            else bv_next = ring_prev[ring_idx(((8 * j + 8) & (kR - 1)) + (lane & 7u), 63)];
                         }
                         if constexpr (DST == 2) {
                             // granules of the previous group (read back from the ring one group ago)
@@ -1052,8 +1115,8 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             gpend = ring_w[ring_idx(8 * j + (lane & 7u), 63)];
                             gpend_t = tg;
                         }
-                        if constexpr (SRC == 2 && j == 3) {
-                            if (lane == 0) st_cons(((uint64_t)ep << 32) | (tg + 8));
+                        if constexpr ((SRC == 2 || (SRC == 1 && kXh)) && j == 3) {
+                            if ((SRC == 2 ? !helped : hpub) && lane == 0) st_cons(((uint64_t)ep << 32) | (tg + 8));
                         }
                     };
                     group(std::integral_constant<uint32_t, 0>{}, sw0);
@@ -1191,13 +1254,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             __hip_atomic_store(x.done + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         const uint32_t f = __hip_atomic_fetch_add(x.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (f == gridDim.x - 1) {  // every workgroup has taken its ticket and read the epoch
-            __hip_atomic_store(x.ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(x.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(x.ctr + 2, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (uint32_t c = kCtrClass; c <= kCtrLeft; ++c)
-                __hip_atomic_store(x.ctr + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (f == gridDim.x - 1) pipe_reset_counters(x);  // every workgroup has taken its ticket
     }
 }
 

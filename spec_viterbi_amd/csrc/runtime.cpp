@@ -851,12 +851,24 @@ void DevicePipePlan::report_stamps(uint32_t nseq) const {
                          w / plan.W, (r[8] - t0) * 0.01, (r[9] - t0) * 0.01, (r[10] - t0) * 0.01, (r[11] - t0) * 0.01);
         }
     }
-    for (uint32_t g = 0; g < plan.G; ++g)
-        for (uint32_t w = 0; w < plan.W; ++w) {
-            const unsigned long long* r = h.data() + ((size_t)g * plan.W + w) * kPipeStamps;
-            std::fprintf(stderr, "  g%u w%u: loop %llu head %llu tail %llu prev %llu next %llu gran %llu cons %llu\n", g, w,
-                         r[0], r[1], r[2], r[3], r[4], r[5], r[6]);
-        }
+    // per-wave counters of sequence 0 and of the sequence whose sweep ends last
+    uint32_t qlast = 0;
+    unsigned long long elast = 0;
+    for (uint32_t q = 0; q < nseq; ++q)
+        for (size_t w = 0; w < (size_t)plan.G * plan.W; ++w)
+            if (h[((size_t)q * plan.G * plan.W + w) * kPipeStamps + 11] > elast) {
+                elast = h[((size_t)q * plan.G * plan.W + w) * kPipeStamps + 11];
+                qlast = q;
+            }
+    for (uint32_t q : {0u, qlast}) {
+        for (uint32_t g = 0; g < plan.G; ++g)
+            for (uint32_t w = 0; w < plan.W; ++w) {
+                const unsigned long long* r = h.data() + (((size_t)q * plan.G + g) * plan.W + w) * kPipeStamps;
+                std::fprintf(stderr, "  seq %u g%u w%u: loop %llu head %llu tail %llu prev %llu next %llu gran %llu cons %llu\n",
+                             q, g, w, r[0], r[1], r[2], r[3], r[4], r[5], r[6]);
+            }
+        if (qlast == 0) break;
+    }
 }
 
 void PipeScratchBuffers::ensure(uint32_t rows, uint32_t G, hipStream_t s) {
