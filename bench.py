@@ -43,7 +43,7 @@ DATA = os.path.join(ROOT, "data")
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_GHZ = 2.4         # MI355X_MICROARCH.md: max shader clock
-KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain", 5: "pipe", 6: "pipew"}
+KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain", 5: "pipe", 6: "pipew", 7: "spec2"}
 
 
 def parse(argv=None):
@@ -261,6 +261,14 @@ def essential_bytes_per_launch(n: int, S: int, lengths, paths: bool, xcds: int =
     kernel's bound (it keeps the model and the scores on chip): reported as bytes only."""
     nseq = len(lengths)
     return sum(lengths) + nseq * n * 4 + nseq * 8 + xcds * S * n * 8 + (4 * sum(lengths) if paths else 0)
+
+
+def spec2_essential_bytes(n: int, S: int, lengths, table_bytes: int, xcds: int = XCDS) -> int:
+    """The same for _spec level 2 on chip (spec2.hip): symbols in, scores and best states out, and
+    once per XCD the plan's term tables (svh_batch_plan spec_bytes) and the emission rows (S x n
+    fp32), which the chunks then re-read from L2."""
+    nseq = len(lengths)
+    return sum(lengths) + nseq * n * 4 + nseq * 8 + xcds * (table_bytes + S * n * 4)
 
 
 def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc, essential_bytes) -> dict:
@@ -535,19 +543,27 @@ def main(argv=None):
         nnz = int(info["nnz"])
         lengths = [int(x.size) for x in seqs]
         algo = algorithmic_bytes_per_launch(n, nnz, lengths, args.level, args.paths)
+        spec2 = args.level == 2 and plan["kernel"] == 7  # level 2 on chip (spec2.hip)
         kname = (KERNEL_NAMES.get(plan["kernel"], "?") + "+traceback" if args.paths
+                 else "spec2 (+ step-kernel tail)" if spec2
                  else "spec_chunk+" + KERNEL_NAMES.get(plan["kernel"], "?") if args.level >= 2
                  else KERNEL_NAMES.get(plan["kernel"], "?"))
         pmc = None
-        if not args.no_pmc and world == 1 and args.level <= 1 and plan["kernel"] in (4, 5, 6):
+        if not args.no_pmc and world == 1 and (args.level <= 1 or spec2) and plan["kernel"] in (4, 5, 6, 7):
             # the dominant kernel's counters (with --paths: the pipelined kernel's PATHS variant, the
-            # pass's dominant kernel; its traceback and the exiting chain launch are not counted)
+            # pass's dominant kernel; its traceback and the exiting chain launch are not counted;
+            # level 2: the on-chip chunk kernel, not the step kernels' one-observation tails)
             largs = ["--model", args.model, "--ess", ess_name, "--replicate", str(args.replicate), "--steps", "3",
-                     "--warmup", "1"] + (["--paths"] if args.paths else [])
-            kpref = {4: "chain_viterbi_kernel", 5: "pipe_viterbi_kernel", 6: "pipew_viterbi_kernel"}[plan["kernel"]]
+                     "--warmup", "1", "--level", str(args.level)] + (["--paths"] if args.paths else [])
+            kpref = {4: "chain_viterbi_kernel", 5: "pipe_viterbi_kernel", 6: "pipew_viterbi_kernel",
+                     7: "spec2_kernel"}[plan["kernel"]]
             pmc = pmc_counters(largs, "void svh::(anonymous namespace)::" + kpref)
-        # level >= 2 streams one dense product per chunk from HBM: those bytes are its bound
-        ess_b = algo if args.level >= 2 else essential_bytes_per_launch(n, int(info["S"]), lengths, args.paths)
+        # level >= 2 on the dense products streams one product per chunk from HBM: those bytes are
+        # its bound; on chip (spec2) the tables are read once per XCD like the step kernels'
+        if spec2:
+            ess_b = spec2_essential_bytes(n, int(info["S"]), lengths, int(plan["spec_bytes"]))
+        else:
+            ess_b = algo if args.level >= 2 else essential_bytes_per_launch(n, int(info["S"]), lengths, args.paths)
         rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc, ess_b)
         workload = (f"{args.model} x {ess_name}" +
                     (f" x{args.replicate} (file sequences + same-shape synthetic copies)" if args.replicate > 1 else "") +

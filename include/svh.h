@@ -71,7 +71,7 @@ void svh_ess_free(svh_ess_t e);
  * is chain-shaped with at most one heavy row feeding the light rows (every reference .chmm), else
  * the fused (or generic) kernel with 16-bit backpointers. */
 enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2, SVH_KERNEL_BAND = 3,
-       SVH_KERNEL_CHAIN = 4, SVH_KERNEL_PIPE = 5, SVH_KERNEL_PIPE_WIDE = 6 };
+       SVH_KERNEL_CHAIN = 4, SVH_KERNEL_PIPE = 5, SVH_KERNEL_PIPE_WIDE = 6, SVH_KERNEL_SPEC2 = 7 };
 /* PIPE: the pipelined chain kernel (MSV-shaped models whose feeder row N takes terms only from
  * the light rows and itself): a sequence's states are split over many waves and CUs; N's light
  * term is speculated away and checked exactly at every observation, and a sequence that fails
@@ -79,7 +79,10 @@ enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2, SVH_KE
  * scores-only passes over batches too small to fill the chip with the chain kernel.
  * PIPE_WIDE: the same recurrence with one block of states per workgroup and one sequence per wave
  * (the block's table in LDS, shared by the waves): the throughput plan AUTO uses for wider
- * batches. */
+ * batches.
+ * SPEC2 (reported by svh_batch_plan only, not selectable): _spec level 2 evaluated on chip from
+ * the folded sparse matrices, one workgroup per sequence (spec2.hip); the odd last observation of
+ * a sequence runs on the step kernels. */
 
 typedef struct {
     int32_t device;      /* HIP device ordinal; -1 = the caller's current device */

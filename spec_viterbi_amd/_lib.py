@@ -32,6 +32,7 @@ SVH_KERNEL_BAND = 3
 SVH_KERNEL_CHAIN = 4
 SVH_KERNEL_PIPE = 5
 SVH_KERNEL_PIPE_WIDE = 6
+SVH_KERNEL_SPEC2 = 7  # svh_batch_plan only: _spec level 2 on chip
 SVH_BATCH_PATHS = 1
 SVH_MODEL_SPEC_DENSE = 1
 

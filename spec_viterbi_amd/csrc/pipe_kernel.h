@@ -138,6 +138,13 @@ constexpr bool kNoWait = true;
 #else
 constexpr bool kNoWait = false;
 #endif
+// Diagnostic ablation (-DSVH_PIPE_NOPSTORE, timing only, wrong paths): the path variant computes
+// and folds its records but stores none of them (tie masks, checkpoints, folded records) to HBM.
+#ifdef SVH_PIPE_NOPSTORE
+constexpr bool kNoPStore = true;
+#else
+constexpr bool kNoPStore = false;
+#endif
 
 // One lane's LDS store of a wave-uniform word (a wave's count): EXEC narrowed to lane 0 inside the
 // asm (no divergent branch in the compiler's view).  Measured and not kept (round 4): every lane
@@ -469,11 +476,13 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         float* const fckq = PATHS ? b.fck + b.fck_off[q] : nullptr;
         const uint32_t wstride = m.nblk * SM * 64;  // mask words per 32 rows
         auto store_masks = [&](uint32_t word, uint32_t rows) {  // rows 32*word .. +rows-1 are in macc
+            if (kNoPStore) return;
 #pragma unroll
             for (int s = 0; s < SM; ++s)
                 cmq[(size_t)word * wstride + (blk * SM + s) * 64 + lane] = macc[s] << (32u - rows);
         };
         auto checkpoint = [&](uint32_t t) {  // t % kCkptEvery == 0: the light scores of t
+            if (kNoPStore) return;
             float* d = ckq + (size_t)(t / kCkptEvery) * m.P + p0;
             if constexpr (SM == 2) {
                 *reinterpret_cast<float2*>(d) = make_float2(v[0], v[1]);
@@ -517,6 +526,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             mm = fminf(mm, __shfl_xor(mm, 32));
             cc = fminf(cc, __shfl_xor(cc, 32));
             const uint32_t tt = tb + o;
+            if (kNoPStore) {
+                asm volatile("" ::"v"(mm), "v"(cc));  // the fold still runs
+                return;
+            }
             if (H == 0 && tt >= 1 && tt < thi) precq[(size_t)blk * len + tt] = make_float2(mm, cc);
         };
         // after the step of observation t (compile-time positions in the unrolled body)

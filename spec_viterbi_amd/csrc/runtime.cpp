@@ -965,6 +965,10 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
     if (dev < 0) hip_check(hipGetDevice(&dev), "hipGetDevice");
     device = dev;
     kernel_pref = opts ? opts->kernel : SVH_KERNEL_AUTO;
+    if (kernel_pref < SVH_KERNEL_AUTO || kernel_pref > SVH_KERNEL_PIPE_WIDE)
+        throw Error(SVH_E_INVALID, "kernel must be one of SVH_KERNEL_AUTO .. SVH_KERNEL_PIPE_WIDE");
+    if (opts && (opts->flags & ~SVH_MODEL_SPEC_DENSE))
+        throw Error(SVH_E_INVALID, "unknown svh_model_opts.flags bits");
     spec_dense = opts && (opts->flags & SVH_MODEL_SPEC_DENSE);
     // 0 = each planner's default; the fused kernel caps at kMaxFusedThreads, the chain kernel at
     // kMaxBandThreads.
@@ -1423,6 +1427,17 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
         i.pipe_groups = (int32_t)pipe.plan.G;
         i.pipe_max_nseq = kernel_pref == SVH_KERNEL_PIPE ? 0xFFFFFFFFu : pipe_max_nseq;
     }
+    if (level == 2 && spec_level == 2 && spec2_on && nseq) {  // the chunks run on chip (spec2.hip)
+        const Spec2Plan& sp = spec2.plan;
+        i.kernel = SVH_KERNEL_SPEC2;
+        i.threads = (int32_t)kSpec2Threads;
+        i.slots = 0;
+        i.light_terms = (int32_t)sp.KL;
+        i.heavy_rows = (int32_t)sp.H;
+        i.lds_bytes = spec2_lds_layout(host.n, sp.KL, sp.NP, sp.H).bytes;
+        i.spec_bytes = spec2.d_la.bytes + spec2.d_lb.bytes + spec2.d_lv.bytes + spec2.d_thr.bytes + spec2.d_tcp.bytes +
+                       spec2.d_ha.bytes + spec2.d_hb.bytes + spec2.d_hv.bytes + spec2.d_hrow.bytes + spec2.d_amax.bytes;
+    }
     return i;
 }
 
@@ -1722,11 +1737,16 @@ void Batch::run(uint32_t level, hipStream_t s) {
         FusedBatch cb = fb;  // chain buffers
         cb.run_mask = pipe.view.viol;
         hip_check(launch_chain(bpl->view, 1, cb, s), "chain Viterbi kernel (pipe paths fallback)");
-        hip_check(launch_pipe_traceback(ppl->view, pb, p_pathoff, d_paths.as<int32_t>(),
-                                        pipe.view.viol, s),
-                  "pipelined traceback kernel");
-        hip_check(launch_chain_traceback(bpl->view, cb, p_pathoff, d_paths.as<int32_t>(), s),
-                  "chain traceback kernel (pipe paths fallback)");
+        // SVH_PIPE_SKIP_TRACEBACK=1: diagnostics only (timing of the forward kernels alone, e.g. of
+        // an ablation build whose path records are not stored; the paths read back are wrong)
+        static const bool skip_tb = std::getenv("SVH_PIPE_SKIP_TRACEBACK") && std::atoi(std::getenv("SVH_PIPE_SKIP_TRACEBACK"));
+        if (!skip_tb) {
+            hip_check(launch_pipe_traceback(ppl->view, pb, p_pathoff, d_paths.as<int32_t>(),
+                                            pipe.view.viol, s),
+                      "pipelined traceback kernel");
+            hip_check(launch_chain_traceback(bpl->view, cb, p_pathoff, d_paths.as<int32_t>(), s),
+                      "chain traceback kernel (pipe paths fallback)");
+        }
         pipe_ran = true;
     } else if (level <= 1) {
         launch_step_kernel(fb, paths);

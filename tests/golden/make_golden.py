@@ -8,6 +8,7 @@ Floats are stored as IEEE-754 bit patterns (hex) so the vectors are exact.
     python tests/golden/make_golden.py digests    # score_digests.json (bench workloads)
     python tests/golden/make_golden.py spec2      # + level-2 digests of every emit_50 row (config 4)
     python tests/golden/make_golden.py scope      # scope_digests.json: every .chmm x emit_3_3500_20
+    python tests/golden/make_golden.py sweep2     # sweep2_digests.json: level 2 of the sweep's other files
 """
 from __future__ import annotations
 
@@ -138,9 +139,55 @@ def scope_digests():
         json.dump({"ess": "emit_3_3500_20.ess", "models": out}, fh, indent=0)
 
 
+SWEEP2_DATASETS = ("emit_3_7000_20.ess", "covid-19.ess", "emit_50_3500_20.ess")
+
+
+def sweep2_digests():
+    """Level-2 score digests of the reference sweep's remaining cells (tools/bench_sweep.py): every
+    .chmm x emit_3_7000_20 / covid-19 / emit_50_3500_20 that score_digests.json does not hold, each
+    model's dense products built once for all three files (one viterbi_spec_batch call).  Written
+    to sweep2_digests.json as {"<model> x <ess> level 2": [sha256 per row]}; resumable (models
+    already in the file are skipped)."""
+    import glob
+    import hashlib
+
+    path = os.path.join(OUT, "sweep2_digests.json")
+    out = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            out = json.load(f)
+    with open(os.path.join(OUT, "score_digests.json")) as f:
+        have = json.load(f)
+    data = {d: svh.read_emit_seq(os.path.join(DATA, "ess_files", d)) for d in SWEEP2_DATASETS}
+    models = sorted(glob.glob(os.path.join(DATA, "chmm_files", "*.chmm")),
+                    key=lambda f: int(os.path.basename(f).split(".")[0]))
+    for f in models:
+        name = os.path.basename(f)
+        todo = [d for d in SWEEP2_DATASETS
+                if f"{name} x {d} level 2" not in have and f"{name} x {d} level 2" not in out]
+        if not todo:
+            continue
+        hmm = svh.read_HMM(f)
+        seqs = [s for d in todo for s in data[d]]
+        scores = oracle.viterbi_spec_batch(hmm, 2, seqs)
+        k = 0
+        for d in todo:
+            rows = []
+            for _ in data[d]:
+                rows.append(hashlib.sha256(np.ascontiguousarray(scores[k], np.float32).tobytes()).hexdigest())
+                k += 1
+            out[f"{name} x {d} level 2"] = rows
+        with open(path, "w") as fh:
+            json.dump(out, fh, indent=0)
+        print("sweep2", name, flush=True)
+
+
 def main():
     if sys.argv[1:] == ["scope"]:
         scope_digests()
+        return
+    if sys.argv[1:] == ["sweep2"]:
+        sweep2_digests()
         return
     if sys.argv[1:] == ["digests"]:
         digests()

@@ -166,6 +166,24 @@ def test_errors():
     with pytest.raises(_lib.SvhError) as e:
         model.viterbi([np.array([0, 1], np.uint64)], level=2)  # spec products not built
     assert e.value.code == _lib.SVH_E_STATE
+    for kw in ({"kernel": _lib.SVH_KERNEL_SPEC2}, {"kernel": -1}, {"flags": 2}):  # not selectable / unknown bits
+        with pytest.raises(_lib.SvhError) as e:
+            svh.DeviceModel(hmm, **kw)
+        assert e.value.code == _lib.SVH_E_INVALID
+
+
+def test_spec2_plan_reported():
+    """svh_batch_plan at level 2 names the on-chip chunk kernel (SVH_KERNEL_SPEC2) with its
+    workgroup size, LDS and table bytes; level 0 of the same batch keeps the step kernel."""
+    hmm = svh.read_HMM(chmm("100.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    model = svh.DeviceModel(hmm)
+    model.spec_build(2)
+    batch = model.batch(seqs)
+    p2, p0 = batch.plan(2), batch.plan(0)
+    assert p2["kernel"] == _lib.SVH_KERNEL_SPEC2 and p2["threads"] == 1024
+    assert p2["lds_bytes"] > 0 and p2["spec_bytes"] > 0 and p2["spec_level"] == 2
+    assert p0["kernel"] != _lib.SVH_KERNEL_SPEC2
 
 
 def test_batch_api_device_resident_rerun():

@@ -107,3 +107,19 @@ def test_path_is_consistent_with_scores():
     for t in range(1, len(seq)):
         acc = np.float32(np.float32(hmm.emissions[seq[t], path[t]] + T[(int(path[t - 1]), int(path[t]))]) + acc)
     assert acc == scores[best]
+
+
+def test_sweep2_digests_reproduce():
+    """tests/golden/sweep2_digests.json (level 2 of the reference sweep's other files, checked by
+    tools/bench_sweep.py on the GPU): the oracle reproduces the first row of a small model's cells."""
+    import hashlib
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "sweep2_digests.json")) as f:
+        d = json.load(f)
+    hmm = svh.read_HMM(chmm("100.chmm"))
+    for name in ("emit_3_7000_20.ess", "covid-19.ess"):
+        seq = svh.read_emit_seq(ess(name))[0]
+        got = hashlib.sha256(np.ascontiguousarray(oracle.viterbi_spec(hmm, 2, seq), np.float32).tobytes()).hexdigest()
+        assert got == d[f"100.chmm x {name} level 2"][0], name
