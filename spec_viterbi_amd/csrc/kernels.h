@@ -221,7 +221,7 @@ struct PipeModel {
     uint32_t diag;               // diagnostics with stamps (SVH_PIPE_DEBUG bits > 1): 1 = no boundary
                                  // exchange (every wave runs as block 0; timing only, wrong results)
 };
-constexpr int kPipeStamps = 13;  // written only by -DSVH_PIPE_DIAG builds of pipe.hip
+constexpr int kPipeStamps = 15;  // written only by -DSVH_PIPE_DIAG builds of pipe.hip
 // Per-batch scratch of the pipelined kernel (sized for `rows` rows).
 constexpr uint32_t kCtrClass = 4, kCtrLeft = 12, kCtrWords = 16;
 struct PipeScratch {

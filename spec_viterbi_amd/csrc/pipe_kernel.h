@@ -130,6 +130,20 @@ __device__ __forceinline__ void wait_vmcnt() {
 #define SVH_PIPE_XHELP 1
 #endif
 
+// Step of a group at which the neighbours' counts (and, SVH_PIPE_EARLYV, the next group's vector)
+// are read (A/B knob SVH_PIPE_CNTSTEP, 1..7): later reads see a producer further ahead, so the next
+// group's vector is valid more often, at the price of less time to hide the LDS latency.  Headline
+// kernel (profiles/r05_xhelp/ab_cntstep.log): step 4 0.2296-0.2329 ms, 5 0.2283-0.2291, 6
+// 0.2284-0.2295, 7 0.243-0.252 (the read's latency no longer hidden).
+#ifndef SVH_PIPE_CNTSTEP
+#define SVH_PIPE_CNTSTEP 5
+#endif
+// (Round 5, measured and not kept: a granule consumer's first boundary awaited alone instead of
+// with the producer's whole first group.  The sweeps start earlier but the rows end no sooner (the
+// workgroup hop's lag is set by the groups' hand-off, not by the start) and the early prefetches
+// poll: 0.2307-0.2323 ms against 0.2291-0.2299, profiles/r05_xhelp/ab_gfirst.log.)
+static_assert(SVH_PIPE_CNTSTEP >= 1 && SVH_PIPE_CNTSTEP <= 7, "count step");
+
 // Diagnostic ablation (-DSVH_PIPE_NOWAIT, timing only, wrong results): every exchange operation
 // runs, but no wait on a neighbour does (counts, flow control, granule tags and progress words are
 // taken as ready): the rate of a wave when no neighbour ever holds it up.
@@ -377,7 +391,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     // diagnostics: 0 loop cycles, 1 head cycles, 2 tail cycles, 3 slow re-reads waiting for the
     // previous wave, 4 ... for the next wave (flow control), 5 ... for granules, 6 ... for the
     // consumer's progress word, 7 body iterations, 8 .. 11 the 100 MHz real-time clock at wave
-    // entry, sweep start, body end, sweep end, 12 the wave's XCC_ID << 32 | HW_ID (placement).
+    // entry, sweep start, body end, sweep end, 12 the wave's XCC_ID << 32 | HW_ID (placement), 13
+    // the real-time clock when the wave's tables have arrived, 14 groups whose boundary vector was
+    // re-read after a wait (the next group's early read not validated).
     // Built only with -DSVH_PIPE_DIAG (tools/ab_build.sh;
     // then SVH_PIPE_DEBUG=1 at run time): the counters would otherwise hold SGPRs through the loop
     // in the production kernel, whose SGPRs are its scarcest register file.
@@ -442,6 +458,13 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 #pragma unroll
             for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(TA[k]), "+v"(TB[k]));
         }
+#ifdef SVH_PIPE_DIAG
+        if (dbg) {  // stamp 13: the tables have arrived (a use of every table register)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) asm volatile("" ::"v"(TA[k]), "v"(TB[k]));
+            SVH_RT(13);
+        }
+#endif
         // heavy constants as lane tables (lane o: symbol o), extracted with v_readlane
         const bool lo = lane < S;
         const float cAS = lo ? m.hc[lane * 8 + 0] : kInf, cAF = lo ? m.hc[lane * 8 + 1] : kInf;
@@ -1056,6 +1079,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             const uint32_t o = (uint32_t)((sw >> (8 * k)) & 0xFFu);
                             if constexpr (SRC == 1 && k == 1) {  // step 0 used only the previous vector
                                 if (!next_ok) {  // the producer had not published this group: wait, re-load
+                                    if (dbg) ++dg[14];
                                     wait_prev(tg + 8);
                                     asm volatile("" ::: "memory");
                                     uint32_t z = 0;  // SVH_PIPE_LDSX: an address the compiler cannot hoist
@@ -1080,7 +1104,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             paths_after(tg + k, std::bool_constant<j == 0 && k == 0>{},
                                         std::bool_constant<k == 0 && (j == 0 || j == 2)>{},
                                         std::bool_constant<j == 3 && k == 7>{}, std::integral_constant<uint32_t, k & 3u>{});
-                            if constexpr (k == 4) {  // the counts checked at the end of the group
+                            if constexpr (k == SVH_PIPE_CNTSTEP) {  // the counts checked at the end of the group
                                 asm volatile("" ::: "memory");
                                 if constexpr (SRC == 1) pc_rd = lds_ld32(cnt_w - 1);
                                 if constexpr (DST == 1) nc_rd = lds_ld32(cnt_w + 1);

@@ -810,9 +810,10 @@ void DevicePipePlan::report_stamps(uint32_t nseq) const {
             mx[k] = std::max(mx[k], (double)h[w * kPipeStamps + k]);
         }
     std::fprintf(stderr, "pipe stamps (avg / max per wave): loop %.0f/%.0f head %.0f/%.0f tail %.0f/%.0f "
-                 "prev %.0f/%.0f next %.0f/%.0f gran %.0f/%.0f cons %.0f/%.0f iters %.0f\n",
+                 "prev %.0f/%.0f next %.0f/%.0f gran %.0f/%.0f cons %.0f/%.0f iters %.0f slow-groups %.0f/%.0f\n",
                  sum[0] / waves, mx[0], sum[1] / waves, mx[1], sum[2] / waves, mx[2], sum[3] / waves, mx[3],
-                 sum[4] / waves, mx[4], sum[5] / waves, mx[5], sum[6] / waves, mx[6], sum[7] / waves);
+                 sum[4] / waves, mx[4], sum[5] / waves, mx[5], sum[6] / waves, mx[6], sum[7] / waves,
+                 sum[14] / waves, mx[14]);
     {  // wall clock (100 MHz): per wave entry / sweep start / body end / sweep end, from the launch's first entry
         unsigned long long t0 = ~0ull, tend = 0;
         for (size_t w = 0; w < waves; ++w)
@@ -825,12 +826,13 @@ void DevicePipePlan::report_stamps(uint32_t nseq) const {
         for (uint32_t q = 0; t0 != ~0ull && q < nseq; ++q) {
             std::fprintf(stderr, "  seq %u:", q);
             for (uint32_t g = 0; g < plan.G; ++g) {
-                unsigned long long en = 0, st = 0, ed = 0;
+                unsigned long long en = 0, st = 0, ed = 0, tb = 0;
                 for (uint32_t w = 0; w < plan.W; ++w) {
                     const unsigned long long* r = h.data() + (((size_t)q * plan.G + g) * plan.W + w) * kPipeStamps;
                     if (!r[8]) continue;
                     en = std::max(en, r[8] - t0);
                     if (w == 0) st = r[9] - t0;
+                    if (w == 0 && r[13]) tb = r[13] - t0;
                     ed = std::max(ed, r[11] - t0);
                 }
                 // placement of the workgroup's first wave: XCC and CU (HW_ID bits 11:8) / SE (14:13)
@@ -838,8 +840,8 @@ void DevicePipePlan::report_stamps(uint32_t nseq) const {
                 const unsigned long long* r0 = h.data() + (((size_t)q * plan.G + g) * plan.W) * kPipeStamps;
                 const unsigned long long hw = r0[12];
                 const double mhz = r0[10] > r0[9] ? (double)r0[0] / ((double)(r0[10] - r0[9]) * 0.01) : 0.0;
-                std::fprintf(stderr, " [g%u in %.1f st %.1f end %.1f x%u s%u c%u %.0fMHz]", g, en * 0.01, st * 0.01,
-                             ed * 0.01, (unsigned)(hw >> 32) & 0xFu, (unsigned)(hw >> 13) & 0x3u,
+                std::fprintf(stderr, " [g%u in %.1f tab %.1f st %.1f end %.1f x%u s%u c%u %.0fMHz]", g, en * 0.01, tb * 0.01,
+                             st * 0.01, ed * 0.01, (unsigned)(hw >> 32) & 0xFu, (unsigned)(hw >> 13) & 0x3u,
                              (unsigned)(hw >> 8) & 0xFu, mhz);
             }
             std::fprintf(stderr, "\n");
@@ -864,8 +866,8 @@ void DevicePipePlan::report_stamps(uint32_t nseq) const {
         for (uint32_t g = 0; g < plan.G; ++g)
             for (uint32_t w = 0; w < plan.W; ++w) {
                 const unsigned long long* r = h.data() + (((size_t)q * plan.G + g) * plan.W + w) * kPipeStamps;
-                std::fprintf(stderr, "  seq %u g%u w%u: loop %llu head %llu tail %llu prev %llu next %llu gran %llu cons %llu\n",
-                             q, g, w, r[0], r[1], r[2], r[3], r[4], r[5], r[6]);
+                std::fprintf(stderr, "  seq %u g%u w%u: loop %llu head %llu tail %llu prev %llu next %llu gran %llu cons %llu slow %llu\n",
+                             q, g, w, r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[14]);
             }
         if (qlast == 0) break;
     }
