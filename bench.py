@@ -210,7 +210,11 @@ PMC_PASSES = {
            "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE"],
     "fetch": ["FETCH_SIZE"],
     "write": ["WRITE_SIZE"],
+    # where waves wait on LDS (optional: a failed pass drops only these counters)
+    "lds": ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS", "SQ_INSTS_LDS_LOAD",
+            "SQ_INSTS_LDS_STORE", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_ADDR_CONFLICT"],
 }
+PMC_OPTIONAL = {"lds"}
 
 
 def pmc_counters(launch_args: list[str], kernel_prefix: str) -> dict | None:
@@ -236,6 +240,8 @@ def pmc_counters(launch_args: list[str], kernel_prefix: str) -> dict | None:
             r = subprocess.run(cmd, capture_output=True, text=True, env=dict(os.environ, TMPDIR="/tmp"))
             if r.returncode != 0:
                 sys.stderr.write(f"bench.py: rocprofv3 pass {name} failed ({r.returncode}): {r.stderr[-500:]}\n")
+                if name in PMC_OPTIONAL:
+                    continue
                 return None
             per: dict[str, dict] = {}
             for f in glob.glob(os.path.join(d, name, "**", "*counter_collection.csv"), recursive=True):
@@ -331,6 +337,16 @@ def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc, essential_bytes) -> d
                 res["cycle_split"] = {k: round(pmc.get(c, 0) / pmc["SQ_WAVE_CYCLES"], 4) for k, c in
                                       (("active_inst", "SQ_ACTIVE_INST_ANY"), ("wait_inst", "SQ_WAIT_INST_ANY"),
                                        ("wait_any", "SQ_WAIT_ANY"))}
+        if "SQ_WAIT_INST_LDS" in pmc and "SQ_WAVE_CYCLES" in pmc:
+            # LDS pass: waves' cycles waiting to issue an LDS instruction, LDS-issue cycles, and the
+            # bank / address conflict cycles per LDS-issue cycle (all per launch, summed over waves)
+            wc = max(pmc["SQ_WAVE_CYCLES"], 1)
+            res["lds"] = {"wait_inst_lds_frac": round(pmc["SQ_WAIT_INST_LDS"] / wc, 4),
+                          "active_inst_lds_frac": round(pmc.get("SQ_ACTIVE_INST_LDS", 0) / wc, 4),
+                          "loads_per_wave": round(pmc.get("SQ_INSTS_LDS_LOAD", 0) / max(pmc.get("SQ_WAVES", 1), 1), 1),
+                          "stores_per_wave": round(pmc.get("SQ_INSTS_LDS_STORE", 0) / max(pmc.get("SQ_WAVES", 1), 1), 1),
+                          "bank_conflict_per_active": round(pmc.get("SQ_LDS_BANK_CONFLICT", 0) / max(pmc.get("SQ_ACTIVE_INST_LDS", 1), 1), 4),
+                          "addr_conflict_per_active": round(pmc.get("SQ_LDS_ADDR_CONFLICT", 0) / max(pmc.get("SQ_ACTIVE_INST_LDS", 1), 1), 4)}
         if "GRBM_GUI_ACTIVE" in pmc:
             res["profiled_clock_ghz"] = round(pmc["GRBM_GUI_ACTIVE"] / 8 / (kernel_ms * 1e6), 3)
     if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:  # KiB; FETCH_SIZE doubled on gfx950

@@ -138,6 +138,11 @@ __device__ __forceinline__ void wait_vmcnt() {
 #ifndef SVH_PIPE_CNTSTEP
 #define SVH_PIPE_CNTSTEP 5
 #endif
+// (Round 5, measured and not kept: the slow path's count and vector reads issued together, one
+// LDS round trip instead of two.  Waves 1-2 of the workgroups fed by granules take that path in
+// 43-67% of their groups; with it cheaper they ran closer to their producer and took it more often
+// (78-97%), for the same kernel time: 0.2300-0.2318 ms against 0.2304-0.2322,
+// profiles/r05_xhelp/ab_slow1.log.)
 // (Round 5, measured and not kept: a granule consumer's first boundary awaited alone instead of
 // with the producer's whole first group.  The sweeps start earlier but the rows end no sooner (the
 // workgroup hop's lag is set by the groups' hand-off, not by the start) and the early prefetches
@@ -1080,10 +1085,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                             if constexpr (SRC == 1 && k == 1) {  // step 0 used only the previous vector
                                 if (!next_ok) {  // the producer had not published this group: wait, re-load
                                     if (dbg) ++dg[14];
-                                    wait_prev(tg + 8);
-                                    asm volatile("" ::: "memory");
                                     uint32_t z = 0;  // SVH_PIPE_LDSX: an address the compiler cannot hoist
                                     if constexpr (SVH_PIPE_LDSX) asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                                    wait_prev(tg + 8);
+                                    asm volatile("" ::: "memory");
                                     bv_next = ring_prev[ring_idx(8 * j + (lane & 7u), 63) + z];
                                 }
                             }

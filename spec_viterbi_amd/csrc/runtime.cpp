@@ -853,6 +853,29 @@ void DevicePipePlan::report_stamps(uint32_t nseq) const {
                          w / plan.W, (r[8] - t0) * 0.01, (r[9] - t0) * 0.01, (r[10] - t0) * 0.01, (r[11] - t0) * 0.01);
         }
     }
+    // the wait split by role: per (workgroup g, wave w) of a row, averaged over the batch's rows:
+    // loop cycles, polls waiting for the previous wave's count (prev), for the next wave's count
+    // (next, flow control), for granules (gran), for the consumer's progress word (cons), and the
+    // groups whose boundary vector was re-read after a wait (slow)
+    {
+        std::fprintf(stderr, "pipe wait split by role (mean over %u rows): g w loop prev next gran cons slow\n", nseq);
+        for (uint32_t g = 0; g < plan.G; ++g)
+            for (uint32_t w = 0; w < plan.W; ++w) {
+                double a[8] = {};
+                uint32_t cnt = 0;
+                for (uint32_t q = 0; q < nseq; ++q) {
+                    const unsigned long long* r = h.data() + (((size_t)q * plan.G + g) * plan.W + w) * kPipeStamps;
+                    if (!r[8]) continue;
+                    ++cnt;
+                    a[0] += (double)r[0];
+                    for (int k = 3; k <= 6; ++k) a[k - 2] += (double)r[k];
+                    a[5] += (double)r[14];
+                }
+                if (!cnt) continue;
+                std::fprintf(stderr, "  role g%u w%u: %.0f %.1f %.1f %.1f %.1f %.1f\n", g, w, a[0] / cnt, a[1] / cnt,
+                             a[2] / cnt, a[3] / cnt, a[4] / cnt, a[5] / cnt);
+            }
+    }
     // per-wave counters of sequence 0 and of the sequence whose sweep ends last
     uint32_t qlast = 0;
     unsigned long long elast = 0;
