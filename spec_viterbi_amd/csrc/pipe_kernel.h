@@ -332,20 +332,22 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     // share an XCD under the observed round-robin placement; speed only -- the hand-offs check the
     // real XCC ids, SVH_PIPE_XL).  Every class r = b % 8 holds n = N / 8 blocks and takes f = n / G
     // rows whole: its k-th ticket (k < f G) is member k % G of row r f + k / G, members numbered in
-    // start order.  The n - f G spare tickets of the classes, in class order, form the remaining
-    // rows (slot u = r (n - f G) + k - f G is member u % G of row 8 f + u / G), so a remaining row
-    // spans at most three classes with two changes (its granule hops cross XCDs only there: each
-    // such hop slowed the rows that took the leftover tickets in start order by a few us); slots and
-    // rows past the batch are dummies that only count themselves finished.
+    // start order.  The n - f G spare tickets of the classes form the remaining rows from one more
+    // counter, also in start order (slot u is member u % G of row 8 f + u / G), so every member's
+    // producer has started before it, whatever the residency.  Those rows span XCDs; with the
+    // exchange helpers their hops cost no more than the others' (class-ordered spare slots, which
+    // kept them to two XCD changes but numbered members across classes out of start order, measured
+    // the same: profiles/r05_xhelp/ab_leftover_start_order.log).  Slots and rows past the batch are
+    // dummies that only count themselves finished.
     if (tid == 0) {
         uint32_t t;
         if (x.xmap) {
-            const uint32_t n = gridDim.x >> 3, r = blockIdx.x & 7u, f = n / G, sp = n - f * G;
+            const uint32_t n = gridDim.x >> 3, r = blockIdx.x & 7u, f = n / G;
             const uint32_t k = __hip_atomic_fetch_add(x.ctr + kCtrClass + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (k < f * G) {
                 t = (r * f + k / G) * G + k % G;
             } else {
-                const uint32_t u = r * sp + (k - f * G);
+                const uint32_t u = __hip_atomic_fetch_add(x.ctr + kCtrLeft, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 t = (8 * f + u / G) * G + u % G;
             }
         } else {
