@@ -138,6 +138,11 @@ __device__ __forceinline__ void wait_vmcnt() {
 #ifndef SVH_PIPE_CNTSTEP
 #define SVH_PIPE_CNTSTEP 5
 #endif
+// (Round 5, measured and not kept: the pair tables' compiler barrier placed after the prologue's
+// other loads, so the heavy constants, the first state and the symbol windows load while the tables
+// are in flight.  The first sweep started later, not earlier (7.2 us after the launch's first entry
+// against 5.9), and the kernel ran 0.2291-0.2301 ms against 0.2272-0.2289,
+// profiles/r05_xhelp/ab_lateopq.log.)
 // (Round 5, measured and not kept: the slow path's count and vector reads issued together, one
 // LDS round trip instead of two.  Waves 1-2 of the workgroups fed by granules take that path in
 // 43-67% of their groups; with it cheaper they ran closer to their producer and took it more often
