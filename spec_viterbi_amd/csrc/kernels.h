@@ -269,10 +269,17 @@ inline uint64_t pipe_ckpt_floats(uint64_t len, uint32_t P) { return len ? ((len 
 inline uint64_t pipe_fck_floats(uint64_t len) { return len ? (len - 1) / 32 + 1 : 0; }
 // LDS of the decoded-path variant beyond pipe_lds_bytes: a ring of 32 rows {pm, c} per wave
 constexpr uint32_t kPRingStride = 132;  // floats per row: 64 lanes x 2 + 4 padding (bank spread)
-// Latency plan (pipe_kernel.h PATHS): per wave 8 quads (4 observations each) of 64 lanes x 8 floats,
-// lanes 32..63 of a quad 128 bytes after lanes 0..31 and quads kPQuadStride floats apart, so the
-// transposed fold (lane = observation, reading 32 lanes' pairs) hits every bank pair at most twice.
-constexpr uint32_t kPQuadStride = 584;  // floats: 64 x 8 + 32 (half gap) + 40 (bank spread)
+// Latency plan (pipe_kernel.h PATHS): per wave 8 quads (4 observations each); a quad is two planes
+// (observations 0-1, 2-3) of 64 lanes x float4, planes kPPlane and quads kPQuadStride floats apart:
+// each 16-byte store of a plane is contiguous over the lanes (conflict-free), and the transposed
+// fold's 32 (quad, observation) addresses for one source lane are 8q + 4 (r / 2) + 2 (r % 2) mod 64
+// dwords, every bank pair once.  (Round 5: the ring's stores cost 50 us of the 0.37 ms path kernel,
+// -DSVH_PIPE_NOPRING; the layout before, lanes' 32 bytes side by side in 584 floats per quad, put
+// each 16-byte store on half the banks.  This layout measured the same -- forward kernels
+// 0.367-0.375 ms against 0.364-0.372, profiles/r05_paths/ab_planar.log -- so the stores' cost is
+// not bank conflicts; kept for its smaller footprint, 16.6 against 18.7 KB per wave.)
+constexpr uint32_t kPPlane = 260;       // floats: 64 x 4 + 4 (260 = 4 mod 64)
+constexpr uint32_t kPQuadStride = 520;  // floats: two planes (520 = 8 mod 64)
 inline size_t pipe_path_lds_bytes(uint32_t W) { return (size_t)W * 8 * kPQuadStride * 4; }
 // Wide pipelined plan (pipe_wide.hip): one block of 64*SM positions per workgroup, W sequences
 // (one per wave), the block's table [nblk][S][NC][64] float4 in LDS (PipeModel.tab; G = nblk);

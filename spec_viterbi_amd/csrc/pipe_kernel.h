@@ -169,6 +169,18 @@ constexpr bool kNoPStore = true;
 #else
 constexpr bool kNoPStore = false;
 #endif
+// Diagnostic ablations (timing only, wrong paths): -DSVH_PIPE_NOFOLD skips the fold of the record
+// ring every 32 observations; -DSVH_PIPE_NOPRING also skips the ring's stores (the step's records).
+#ifdef SVH_PIPE_NOFOLD
+constexpr bool kNoFold = true;
+#else
+constexpr bool kNoFold = false;
+#endif
+#ifdef SVH_PIPE_NOPRING
+constexpr bool kNoPRing = true;
+#else
+constexpr bool kNoPRing = false;
+#endif
 
 // One lane's LDS store of a wave-uniform word (a wave's count): EXEC narrowed to lane 0 inside the
 // asm (no divergent branch in the compiler's view).  Measured and not kept (round 4): every lane
@@ -502,8 +514,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 
         // ---- decoded paths: outputs and the per-slot tie masks
         float* const pring_w = pring + w * 8 * kPQuadStride;
-        // lane l's 32 bytes in quad q (observations 4q..4q+3 of the cycle of 32)
-        float* const pring_l = pring_w + lane * 8 + (lane >= 32 ? 32 : 0);
+        // lane l's float4 in plane 0 of quad q (observations 4q, 4q+1 of the cycle of 32; plane 1,
+        // kPPlane floats on, holds 4q+2, 4q+3)
+        float* const pring_l = pring_w + lane * 4;
         float pst[8];  // this quad's {pm, c} pairs, written by two ds_write_b128 at its last step
         uint32_t* const cmq = PATHS ? b.cmask + b.cmask_off[q] : nullptr;
         float* const ckq = PATHS ? b.ckpt + b.ckpt_off[q] : nullptr;
@@ -536,25 +549,31 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             pst[2 * r + 1] = CF.x;
         };
         auto ring_flush = [&](uint32_t t) {  // t % 4 == 3: the quad of t is complete
-            float4* d = reinterpret_cast<float4*>(pring_l + ((t >> 2) & 7u) * kPQuadStride);
-            d[0] = make_float4(pst[0], pst[1], pst[2], pst[3]);
-            d[1] = make_float4(pst[4], pst[5], pst[6], pst[7]);
+            if (kNoPRing) {
+                asm volatile("" ::"v"(pst[0]), "v"(pst[1]), "v"(pst[2]), "v"(pst[3]), "v"(pst[4]), "v"(pst[5]), "v"(pst[6]), "v"(pst[7]));
+                return;
+            }
+            float* d = pring_l + ((t >> 2) & 7u) * kPQuadStride;
+            *reinterpret_cast<float4*>(d) = make_float4(pst[0], pst[1], pst[2], pst[3]);
+            *reinterpret_cast<float4*>(d + kPPlane) = make_float4(pst[4], pst[5], pst[6], pst[7]);
         };
         auto ring_put1 = [&](uint32_t t) {
-            *reinterpret_cast<float2*>(pring_l + ((t >> 2) & 7u) * kPQuadStride + (t & 3u) * 2) = make_float2(last_pm, CF.x);
+            *reinterpret_cast<float2*>(pring_l + ((t >> 2) & 7u) * kPQuadStride + ((t & 3u) >> 1) * kPPlane + (t & 1u) * 2) =
+                make_float2(last_pm, CF.x);
         };
         // fold observations tb .. tb+31 (tb % 32 == 0) and store those in [1, thi): lane l takes
         // observation o = l % 32 over the half-wave of source lanes l / 32, then the two halves
         // combine (one swizzle) and lanes 0..31 store one record per observation
         auto reduce_ring = [&](uint32_t tb, uint32_t thi) {
+            if (kNoFold || kNoPRing) return;
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
             const uint32_t o = lane & 31u, H = lane >> 5;
-            const float* rp = pring_w + (o >> 2) * kPQuadStride + H * (32 * 8 + 32) + (o & 3u) * 2;
+            const float* rp = pring_w + (o >> 2) * kPQuadStride + ((o & 3u) >> 1) * kPPlane + H * (32 * 4) + (o & 1u) * 2;
             float mm = kInf, cc = kInf;
 #pragma unroll
             for (int L = 0; L < 32; ++L) {
-                const float2 e = *reinterpret_cast<const float2*>(rp + L * 8);
+                const float2 e = *reinterpret_cast<const float2*>(rp + L * 4);
                 mm = fminf(mm, e.x);
                 cc = fminf(cc, e.y);
             }
