@@ -18,7 +18,7 @@ HOSTFLAGS := --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wa
 
 HIP_SRCS  := $(wildcard $(CSRC)/fused_*.hip) $(CSRC)/misc.hip $(CSRC)/band.hip $(wildcard $(CSRC)/chain_*.hip) $(CSRC)/timepar.hip $(CSRC)/pipe.hip \
              $(CSRC)/pipe_tm1.hip $(CSRC)/pipe_tm1p.hip $(CSRC)/pipe_wide.hip $(CSRC)/pipe_wide_paths.hip $(CSRC)/pipe_paths.hip \
-             $(CSRC)/spec2.hip
+             $(CSRC)/spec2.hip $(CSRC)/pipe_l2.hip
 HOST_SRCS := $(CSRC)/runtime.cpp $(CSRC)/svh_api.cpp $(CSRC)/HIP_impl.cpp $(CSRC)/data_reader.cpp $(CSRC)/stream.cpp \
              $(CSRC)/seqreader.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS))
@@ -49,7 +49,7 @@ $(LIB): $(OBJS) $(BUILD)/pipe.hazards
 
 # The pipelined kernel's inline-asm DPP reads rely on the schedule for one of their two wait
 # states: every build checks all of them in the gfx950 code objects (tools/dpp_hazards.py).
-PIPE_OBJS := pipe pipe_tm1 pipe_tm1p
+PIPE_OBJS := pipe pipe_tm1 pipe_tm1p pipe_l2
 $(BUILD)/pipe.hazards: $(foreach o,$(PIPE_OBJS),$(BUILD)/$(o).o) tools/dpp_hazards.py
 	set -e; for o in $(PIPE_OBJS); do \
 	  (cd $(BUILD) && /opt/rocm/lib/llvm/bin/llvm-objdump --offloading $$o.o > /dev/null); \

@@ -43,7 +43,7 @@ DATA = os.path.join(ROOT, "data")
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_GHZ = 2.4         # MI355X_MICROARCH.md: max shader clock
-KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain", 5: "pipe", 6: "pipew", 7: "spec2"}
+KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain", 5: "pipe", 6: "pipew", 7: "spec2", 8: "spec2-pipe"}
 
 
 def parse(argv=None):
@@ -217,7 +217,7 @@ PMC_PASSES = {
 PMC_OPTIONAL = {"lds"}
 
 
-def pmc_counters(launch_args: list[str], kernel_prefix: str) -> dict | None:
+def pmc_counters(launch_args: list[str], kernel_prefix: str, kernel_suffix: str = "") -> dict | None:
     """Per-launch counters of the dominant kernel from separate rocprofv3 --pmc passes over
     tools/launch.py (same workload), or None when rocprofv3 is unavailable or a pass fails."""
     import csv
@@ -247,7 +247,8 @@ def pmc_counters(launch_args: list[str], kernel_prefix: str) -> dict | None:
             for f in glob.glob(os.path.join(d, name, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
-                        if not row.get("Kernel_Name", "").startswith(kernel_prefix):
+                        kn = row.get("Kernel_Name", "")
+                        if not kn.startswith(kernel_prefix) or (kernel_suffix and kernel_suffix not in kn):
                             continue
                         per.setdefault(row["Counter_Name"], {}).setdefault(row["Dispatch_Id"], 0.0)
                         per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"] or 0)
@@ -288,7 +289,7 @@ def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc, essential_bytes) -> d
     wave's issue slot the same way (its bound at one wave per SIMD).  The wide pipelined kernel runs
     ceil(nseq / W) x pipew_blocks workgroups of W waves (threads / 64), one per CU (its LDS)."""
     waves_per_wg = max(1, int(plan["threads"]) // 64)
-    pipe = plan["kernel"] == 5
+    pipe = plan["kernel"] in (5, 8)  # 8: level 2 on the pipelined latency plan (same geometry)
     wide = plan["threads"] == info.get("wide_threads") and plan["slots"] == info.get("wide_slots") and nseq > info["cu_count"]
     wg_per_cu = 4 if wide else 1  # launch-bounds occupancy of the wide plan; one WG per CU otherwise
     pipew = plan["kernel"] == 6
@@ -461,7 +462,10 @@ def main(argv=None):
         model.spec_build(args.level)
         torch.cuda.synchronize()
         prep_s = time.perf_counter() - t_prep
-    batch = model.batch(seqs, paths=args.paths) if seqs else None
+    # timing=False: the batch records no events of its own in run() (SVH_BATCH_NO_TIMING): each event
+    # record is a marker the next kernel waits behind, ~3 us on MI355X; the timed region below is
+    # bracketed by one pair of events on the run's stream instead of a pair per step
+    batch = model.batch(seqs, paths=args.paths, timing=False) if seqs else None
     plan = batch.plan(args.level) if batch else info
     # A stream of our own: torch's default stream has handle 0, which the C ABI reads as "the
     # model's own stream", so events recorded on torch's default stream would not bracket the
@@ -475,19 +479,22 @@ def main(argv=None):
             batch.run(args.level, sptr)
     torch.cuda.synchronize()
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    stops = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # HIP events on the stream the kernels run on, bracketing the K timed passes (one record before
+    # the first, one after the last: per-step records would put 2 K markers into the timed stream);
+    # kernel_ms = that span / K, the average pass on the device, launch gaps included
+    ev_start = torch.cuda.Event(enable_timing=True)
+    ev_stop = torch.cuda.Event(enable_timing=True)
     barrier(world, args)
     t0 = time.perf_counter()
+    ev_start.record(stream)
     for k in range(args.steps):
-        starts[k].record(stream)
         if batch:
             batch.run(args.level, sptr)
-        stops[k].record(stream)
+    ev_stop.record(stream)
     torch.cuda.synchronize()
     barrier(world, args)
     elapsed = max_over_ranks(time.perf_counter() - t0, world, local, args)
-    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, stops)]))
+    kernel_ms = float(ev_start.elapsed_time(ev_stop)) / max(args.steps, 1)
 
     scores, best = batch.read(sptr) if batch else (np.zeros((0, n), np.float32), np.zeros(0, np.int64))
     # rows of the last timed pass the pipelined kernel handed to the serial kernel (0 expected)
@@ -560,20 +567,24 @@ def main(argv=None):
         lengths = [int(x.size) for x in seqs]
         algo = algorithmic_bytes_per_launch(n, nnz, lengths, args.level, args.paths)
         spec2 = args.level == 2 and plan["kernel"] == 7  # level 2 on chip (spec2.hip)
+        l2pipe = args.level == 2 and plan["kernel"] == 8  # level 2 on the pipelined latency plan
         kname = (KERNEL_NAMES.get(plan["kernel"], "?") + "+traceback" if args.paths
                  else "spec2 (+ step-kernel tail)" if spec2
+                 else "spec2-pipe (pipelined level-2 chunks + step-kernel tail)" if l2pipe
                  else "spec_chunk+" + KERNEL_NAMES.get(plan["kernel"], "?") if args.level >= 2
                  else KERNEL_NAMES.get(plan["kernel"], "?"))
         pmc = None
-        if not args.no_pmc and world == 1 and (args.level <= 1 or spec2) and plan["kernel"] in (4, 5, 6, 7):
+        if not args.no_pmc and world == 1 and (args.level <= 1 or spec2 or l2pipe) and plan["kernel"] in (4, 5, 6, 7, 8):
             # the dominant kernel's counters (with --paths: the pipelined kernel's PATHS variant, the
             # pass's dominant kernel; its traceback and the exiting chain launch are not counted;
             # level 2: the on-chip chunk kernel, not the step kernels' one-observation tails)
             largs = ["--model", args.model, "--ess", ess_name, "--replicate", str(args.replicate), "--steps", "3",
                      "--warmup", "1", "--level", str(args.level)] + (["--paths"] if args.paths else [])
             kpref = {4: "chain_viterbi_kernel", 5: "pipe_viterbi_kernel", 6: "pipew_viterbi_kernel",
-                     7: "spec2_kernel"}[plan["kernel"]]
-            pmc = pmc_counters(largs, "void svh::(anonymous namespace)::" + kpref)
+                     7: "spec2_kernel", 8: "pipe_viterbi_kernel"}[plan["kernel"]]
+            # level 2 on the pipelined plan: its L2 instantiation (template argument L2 = true), not the
+            # step kernel's one-observation tails that share the name
+            pmc = pmc_counters(largs, "void svh::(anonymous namespace)::" + kpref, ", true>" if l2pipe else "")
         # level >= 2 on the dense products streams one product per chunk from HBM: those bytes are
         # its bound; on chip (spec2) the tables are read once per XCD like the step kernels'
         if spec2:

@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define SVH_ABI_VERSION 2  /* 2: svh_model_info pipe_* fields, SVH_KERNEL_PIPE, svh_batch_fallbacks */
+#define SVH_ABI_VERSION 3  /* 2: svh_model_info pipe_* fields, SVH_KERNEL_PIPE, svh_batch_fallbacks;
+                              3: pipe_max_nseq_paths, SVH_KERNEL_SPEC2_PIPE, SVH_BATCH_NO_TIMING */
 
 enum {
     SVH_OK = 0,
@@ -71,7 +72,8 @@ void svh_ess_free(svh_ess_t e);
  * is chain-shaped with at most one heavy row feeding the light rows (every reference .chmm), else
  * the fused (or generic) kernel with 16-bit backpointers. */
 enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2, SVH_KERNEL_BAND = 3,
-       SVH_KERNEL_CHAIN = 4, SVH_KERNEL_PIPE = 5, SVH_KERNEL_PIPE_WIDE = 6, SVH_KERNEL_SPEC2 = 7 };
+       SVH_KERNEL_CHAIN = 4, SVH_KERNEL_PIPE = 5, SVH_KERNEL_PIPE_WIDE = 6, SVH_KERNEL_SPEC2 = 7,
+       SVH_KERNEL_SPEC2_PIPE = 8 };
 /* PIPE: the pipelined chain kernel (MSV-shaped models whose feeder row N takes terms only from
  * the light rows and itself): a sequence's states are split over many waves and CUs; N's light
  * term is speculated away and checked exactly at every observation, and a sequence that fails
@@ -132,6 +134,9 @@ typedef struct {
     int32_t pipew_waves;   /* ... sequences (waves) per workgroup */
     int32_t pipew_blocks;  /* ... workgroups per sequence */
     uint32_t pipew_min_nseq; /* AUTO runs it for batches of at least this many sequences */
+    uint32_t pipe_max_nseq_paths; /* ... the latency plan's bound for decoded-path batches (one
+                                     workgroup per CU; pipe_max_nseq allows two for scores; the
+                                     SVH_PIPE_MAX_NSEQ override applies to scores only) */
 } svh_model_info;
 /* The model's plan for a one-sequence scores-only run (kernel/threads/slots describe it). */
 int svh_model_get_info(svh_model_t m, svh_model_info* info);
@@ -144,7 +149,10 @@ int svh_model_get_info(svh_model_t m, svh_model_info* info);
 int svh_spec_build(svh_model_t m, uint32_t level, void* stream);
 
 /* ---- batches: sequences resident in HBM ------------------------------------------------ */
-enum { SVH_BATCH_PATHS = 1 };
+/* SVH_BATCH_PATHS: decoded paths.  SVH_BATCH_NO_TIMING: svh_batch_run records no start / stop
+ * events on the stream (svh_batch_elapsed_ms then fails with SVH_E_STATE); for callers that time
+ * the stream themselves -- each event record is a marker the next kernel waits behind. */
+enum { SVH_BATCH_PATHS = 1, SVH_BATCH_NO_TIMING = 2 };
 
 /* offsets: nseq + 1 prefix offsets into symbols; every sequence must be non-empty. */
 int svh_batch_create(svh_model_t m, uint64_t nseq, const uint64_t* offsets,

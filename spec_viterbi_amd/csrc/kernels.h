@@ -210,6 +210,11 @@ struct PipeModel {
     uint32_t sx;            // S has a term from F
     uint32_t tm;            // latency plan's table mode (pipe_kernel.h): 1 = pair tables (SM = 2, S <= 20)
     uint32_t wide;          // 1: the wide plan's geometry and table layout (pipe_wide_kernel.h)
+    float emax2;            // _spec level 2 on this plan (pipe_l2.hip): the largest finite ea over
+                            // positions and symbols (its margin check), +inf: level 2 not supported
+    uint32_t rerun;         // latency plan, scores: a row whose speculation fails is re-run exactly by
+                            // its combining workgroup (pipe_rerun_row; needs 2P + 2W floats of the ring's
+                            // LDS), so no fallback launch follows the pass; 0: the host launches one
     // decoded paths (pipe PATHS variant + pipe_traceback_kernel):
     const uint8_t* pflags;  // [P] bit0: term from position p-1 exists, bit1: term from F exists,
                             // bit2: F's row < row of p-1 (F wins ties)
@@ -241,12 +246,21 @@ __host__ __device__ inline size_t pipe_lds_bytes(uint32_t W, uint32_t S) {
     // boundary ring [W][kPipeRing][64] | counters [16] | heavy constants [S][8] | reduction [W][4] | ticket
     return ((size_t)W * kPipeRing * 64 + 16 + (size_t)S * 8 + (size_t)W * 4 + 4) * 4;
 }
+// The latency plan's in-kernel re-run (PipeModel::rerun) keeps v[2][P] and red[2][W] in the ring.
+__host__ __device__ inline bool pipe_rerun_fits(uint32_t P, uint32_t W) {
+    return 2ull * P + 2ull * W <= (size_t)W * kPipeRing * 64;
+}
 bool pipe_supported(int sm, int waves, bool sx);
 // table mode tm (pipe_kernel.h TM) compiled into this build at the default geometry (TM 1..3 and
 // the other geometries only in SVH_PIPE_AB_ALL builds)
 bool pipe_tm_supported(int tm);
 // b.cmask != nullptr selects the decoded-path variant (every sequence must start at step 0).
 hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
+// _spec level 2 on the latency plan's geometry (pipe_l2.hip: pipe_kernel.h with L2): every chunk of
+// two observations of every row, from observation 0, into b.scores (dense rows; best states when
+// b.best); rows whose speculation fails are flagged in x.viol (re-run by spec2_kernel, runtime.cpp).
+hipError_t launch_pipe_l2(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
+bool pipe_l2_supported(const PipeModel& m);
 bool pipe_paths_supported(int sm, int waves);
 // Decoded paths of the pipelined plan: the records {F, C, mu} from the per-block partials, then
 // the path walk (pipe_paths.hip); rows with skip[q] != 0 (re-run by the chain kernel) are left
@@ -432,6 +446,8 @@ struct Spec2Batch {
     const uint32_t* nchunks;  // [nseq] floor((len - 1) / 2)
     float* v;                 // [nseq][n] in: the state after observation 0; out: after the chunks
     uint32_t nseq;
+    const uint32_t* run_mask = nullptr;  // rows with run_mask[q] == 0 return at once (nullptr: all)
+    float* v_out = nullptr;              // [nseq][n] out instead of v (nullptr: in place)
 };
 struct Spec2Lds {
     uint32_t v, pairs, hacc, cmin, ccnt, eh, amax;  // offsets in floats (16-byte aligned)

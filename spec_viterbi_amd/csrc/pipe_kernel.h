@@ -315,6 +315,16 @@ struct ChainIn {
     float b;
 };
 
+// Lanes 1..63 take v of lane - 1 (DPP wave_shr:1); lane 0 takes lane R of bvv (row_ror:16-R; R = 0:
+// lane 0's own bvv, which is also the form for a uniform boundary).  Built from the DPP builtins, so
+// the compiler inserts the wait states (the level-2 step, L2 below).
+template <int R>
+__device__ __forceinline__ float shr_in(float v, float bvv) {
+    int old = __builtin_bit_cast(int, bvv);
+    if constexpr (R > 0) old = __builtin_amdgcn_update_dpp(old, old, 0x120 + (16 - R), 0xf, 0xf, false);
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(old, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+
 // The last workgroup of a launch to finish (every one has taken its ticket and read the epoch):
 // tickets and the finish count back to 0, the epoch advanced (ctr[2] + 1 is this launch's).
 __device__ __forceinline__ void pipe_reset_counters(const PipeScratch& x) {
@@ -325,10 +335,122 @@ __device__ __forceinline__ void pipe_reset_counters(const PipeScratch& x) {
     __hip_atomic_store(x.ctr + 2, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int SM, int W, bool SX, int PATHS, int TM>
+// Exact serial re-run of row q whose speculation failed (m.rerun: the scores variant of the latency
+// plan, P small enough for the ring's LDS), by the workgroup that combines the row, so that no
+// second launch is needed on the common path (round 5 launched the serial chain kernel after every
+// pass, 4.1 us of 50 workgroups that exit at once).  The recurrence is the one the sweep speculates
+// on, with F's light term restored (GraphBLAS_impl.cpp:64-73, the association of chain_impl.h):
+//   v'_p = min(fl(eb_p(o) + v_{p-1}), fl(ea_p(o) + F)),   F' = min(fl(A_F + mu), fl(X_FF + F)),
+//   C'   = min(fl(A_S + mu), fl(X_SS + C) [, fl(X_SF + F)]),   mu = min_p v_p (scores of t-1).
+// Scores double-buffered in LDS (v[2][P], position-major), thread i updates positions i, i + T, ...
+// (the table reads coalesce), per-wave minima in red[2][W]; one barrier per observation.  Slow
+// (~2 us per observation) but only for rows that fail the check, which no reference workload does.
+template <int SM, int W, bool SX>
+__device__ __forceinline__ void pipe_rerun_row(const PipeModel& m, const FusedBatch& b, uint32_t q, float* lds) {
+    constexpr uint32_t T = 64 * W;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t P = m.P, S = m.S;
+    float* vb = lds;                       // [2][P]
+    float* red = lds + 2 * P;              // [2][W]
+    const uint8_t* __restrict__ sym = b.symbols + b.sym_off[q];
+    const uint32_t len = (uint32_t)uniform((int)b.end[q]);
+    const uint32_t beg = (uint32_t)uniform((int)b.begin[q]);
+    const uint32_t first = beg ? beg : 1u;
+    float F, C;
+    float mu = kInf;
+    // state at observation first - 1
+    if (beg == 0) {
+        const uint32_t o0 = sym[0];
+        for (uint32_t p = tid; p < P; p += T) {
+            const float v = m.e0[(size_t)o0 * P + p] + m.start[p];
+            vb[p] = v;
+            mu = fminf(mu, v);
+        }
+        F = m.rowF >= 0 ? m.hc[o0 * 8 + 5] + m.startF : kInf;
+        C = m.rowS >= 0 ? m.hc[o0 * 8 + 6] + m.startS : kInf;
+    } else {
+        const float* vin = b.v_in + (size_t)b.v_in_row[q] * m.n;
+        for (uint32_t p = tid; p < P; p += T) {
+            const uint32_t r = m.lrow[p];
+            const float v = r != kNoRow ? vin[r] : kInf;
+            vb[p] = v;
+            mu = fminf(mu, v);
+        }
+        F = m.rowF >= 0 ? vin[m.rowF] : kInf;
+        C = m.rowS >= 0 ? vin[m.rowS] : kInf;
+    }
+    mu = wave_min63(mu);
+    if (lane == 63) red[w] = mu;
+    __syncthreads();
+    uint32_t cur = 0;
+    for (uint32_t t = first; t < len; ++t) {
+        const uint32_t o = (uint32_t)uniform((int)sym[t]);
+        float m0 = kInf;
+#pragma unroll
+        for (int u = 0; u < W; ++u) m0 = fminf(m0, red[cur * W + u]);
+        const float4 h = *reinterpret_cast<const float4*>(m.hc + o * 8);  // A_S A_F X_SS X_FF
+        const float Fn = fminf(h.y + m0, h.w + F);
+        float Cn = fminf(h.x + m0, h.z + C);
+        if constexpr (SX) Cn = fminf(Cn, m.hc[o * 8 + 4] + F);
+        const float* vc = vb + cur * P;
+        float* vn = vb + (cur ^ 1u) * P;
+        float mn = kInf;
+        for (uint32_t p = tid; p < P; p += T) {
+            // position p = (blk, lane l, slot s) of the sweep's layout: tab[((blk S + o) SM + s) 64 + l]
+            const uint32_t blk = p / (64 * SM), r = p - blk * 64 * SM, l = r / SM, s = r - l * SM;
+            const float2 e = m.tab[((size_t)(blk * S + o) * SM + s) * 64 + l];
+            const float prev = p ? vc[p - 1] : kInf;
+            const float v = fminf(e.x + prev, e.y + F);
+            vn[p] = v;
+            mn = fminf(mn, v);
+        }
+        mn = wave_min63(mn);
+        if (lane == 63) red[(cur ^ 1u) * W + w] = mn;
+        F = Fn;
+        C = Cn;
+        cur ^= 1u;
+        __syncthreads();
+    }
+    // scores, best state (lexicographic (value, row) argmin, lowest row on ties)
+    float* out = b.scores + (size_t)q * m.n;
+    const float* vc = vb + cur * P;
+    float bv = kInf;
+    uint32_t bk = kNoRow;
+    for (uint32_t p = tid; p < P; p += T) {
+        const uint32_t r = m.lrow[p];
+        if (r != kNoRow) {
+            out[r] = vc[p];
+            lex_min(bv, bk, vc[p], r);
+        }
+    }
+    wave_lexmin63(bv, bk);
+    __syncthreads();  // every wave has read vc and red
+    if (lane == 63) {
+        red[2 * w] = bv;
+        red[2 * w + 1] = __builtin_bit_cast(float, bk);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float v2 = kInf;
+        uint32_t k2 = kNoRow;
+        for (uint32_t u = 0; u < (uint32_t)W; ++u) lex_min(v2, k2, red[2 * u], __builtin_bit_cast(uint32_t, red[2 * u + 1]));
+        if (m.rowF >= 0) {
+            out[m.rowF] = F;
+            lex_min(v2, k2, F, (uint32_t)m.rowF);
+        }
+        if (m.rowS >= 0) {
+            out[m.rowS] = C;
+            lex_min(v2, k2, C, (uint32_t)m.rowS);
+        }
+        if (b.best) b.best[q] = k2 == kNoRow ? -1 : (int64_t)k2;
+    }
+}
+
+template <int SM, int W, bool SX, int PATHS, int TM, bool L2 = false>
 __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     static_assert(TM == 0 || SM == 2, "pair tables: two slots per lane");
     static_assert(TM >= 0 && TM <= 4, "table mode");
+    static_assert(!L2 || (SM == 2 && TM == 4 && PATHS == 0 && SVH_PIPE_RING8), "level 2: the pair-table scores kernel");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* ring = lds;                                                  // [W][kR][64]
     uint32_t* cnt = reinterpret_cast<uint32_t*>(ring + W * kR * 64);    // [16]
@@ -392,8 +514,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 #endif
 
     const uint8_t* __restrict__ sym = b.symbols + b.sym_off[q];
-    const uint32_t len = (uint32_t)uniform((int)b.end[q]);
-    const uint32_t beg = (uint32_t)uniform((int)b.begin[q]);
+    // L2: the sweep's t runs over observations 1 .. 2 nch of the nch = (L - 1) / 2 chunks (every row
+    // starts at observation 0; the odd tail is the step kernel's, runtime.cpp)
+    const uint32_t len = L2 ? 1u + (((uint32_t)uniform((int)b.end[q]) - 1u) & ~1u) : (uint32_t)uniform((int)b.end[q]);
+    const uint32_t beg = L2 ? 0u : (uint32_t)uniform((int)b.begin[q]);
     const uint32_t first = beg ? beg : 1u;  // first observation the steps run (state at first-1)
     const uint32_t blk = g * W + w;
     const bool act = blk < m.nblk;
@@ -454,9 +578,38 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         // mode 3: the pair-interleaved tables (symbols >= S: +inf)
         constexpr bool kT3 = TM >= 1;  // pair tables (symbols pre-doubled)
         constexpr bool kT4 = TM == 1 || TM == 3;  // ... read by four 64-bit moves
-        f32x32 TA[4];
-        f32x8 TB[4];
-        if constexpr (kT3) {
+        constexpr int NT = 4;
+        f32x32 TA[NT];
+        f32x8 TB[NT];
+        if constexpr (L2) {
+            // level 2 (three pair tables, register 2o + u of table k = value u of symbol o):
+            // T0 {eb_0, eb_1}, T1 {ea_0, ea_1}, T2 {eb, ea} of position p0 - 1 (lane - 1's slot 1, the
+            // previous block's last position for lane 0; +inf before block 0).  The heavy constants
+            // come from the lane tables by v_readlane: six pinned tables (240 registers) left the
+            // step 14 of the 256 architectural VGPRs (the first build spilled 567 registers)
+#pragma unroll
+            for (int o = 0; o < (int)kPairSym; ++o) {
+                const bool ok = (uint32_t)o < S;
+                const uint32_t oc = ok ? (uint32_t)o : S - 1u;
+                const float2 e0 = m.tab[((size_t)(blk * S + oc) * SM + 0) * 64 + lane];
+                const float2 e1 = m.tab[((size_t)(blk * S + oc) * SM + 1) * 64 + lane];
+                const uint32_t pb = lane ? blk : (blk ? blk - 1u : 0u), pl = lane ? lane - 1u : 63u;
+                const bool pok = ok && (lane || blk);
+                const float2 pe = m.tab[((size_t)(pb * S + oc) * SM + 1) * 64 + pl];
+                const float val[3][2] = {{ok ? e0.x : kInf, ok ? e1.x : kInf}, {ok ? e0.y : kInf, ok ? e1.y : kInf},
+                                         {pok ? pe.x : kInf, pok ? pe.y : kInf}};
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int r = 2 * o + u;
+                        if (r < 32) TA[k][r] = val[k][u];
+                        else TB[k][r - 32] = val[k][u];
+                    }
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) asm volatile("" : "+v"(TA[k]), "+v"(TB[k]));
+        } else if constexpr (kT3) {
 #pragma unroll
             for (int o = 0; o < (int)kPairSym; ++o) {
                 const bool ok = (uint32_t)o < S;
@@ -849,6 +1002,104 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             for (int s = 0; s < SM; ++s) v[s] = vn[s];
         };
 
+        // ---- L2: one chunk of _spec level 2 (observations t - 1, t with symbols s1, s2; o1, o2 = 2 x
+        // the symbols).  GraphBLAS_spec_impl.cpp:15-36, 66-81: v'[j] = min_m fl(H[j][m] + v[m]) with
+        // H[j][m] = min_p fl(M_s2[j][p] + M_s1[p][m]), M_s[j][p] = fl(E_s[j] + T^T[j][p]); fl(x + v) is
+        // monotone in x, so bit for bit v'[j] = min over the two-hop paths j <- p <- m of
+        // fl(fl(M_s2[j][p] + M_s1[p][m]) + v[m]) (spec2.hip (1)).  In the chain shape the paths into a
+        // light position j are (j-1, j-2), (j-1, F), (F, F) and (F, light m); into F: (F, F), (F, m),
+        // (q, q-1), (q, F) for every light q; into S: (S, S), (S, m), (q, q-1), (q, F) [+ (S, F),
+        // (F, F), (F, m) with SX].  So, with eb/ea the folded tables of level 0:
+        //   v'_j = min(fl(fl(eb_j(s2) + eb_{j-1}(s1)) + v_{j-2}),
+        //              fl(min(fl(eb_j(s2) + ea_{j-1}(s1)), fl(ea_j(s2) + X_FF(s1))) + F))     [exact]
+        //          and the (F, m) term fl(fl(ea_j(s2) + A_F(s1)) + mu), which is speculated never to win;
+        //   F' = fl(fl(X_FF(s2) + X_FF(s1)) + F), speculated: every other term of F checked >= F' exactly
+        //        in the lane that holds it ((F, m) with the lane's own minimum: fl(a + .) is monotone);
+        //   S: every term evaluated in the lane that holds it, S = min over lanes (as at level 0).
+        // The two light positions two apart form independent chains (even and odd), each depending on
+        // position j - 2 of the previous chunk: lane - 1's same slot, the previous block's last two
+        // scores for lane 0.  The speculated (F, m) term of position j is bounded without mu: with all
+        // scores >= 0 (the host's check) each fl() is within (1 +- u) of the exact sum, so
+        // fl(fl(e + A_F) + mu) >= fl(fl(e + X_FF) + F) for every e in [0, emax2] once
+        // fl(A_F + mu_lane) >= fl(R + fl(emax2 + R) 2^-20), R = fl(X_FF + F): the margin 16u (emax2 + R)
+        // exceeds the 4u (e + X_FF + F) the four roundings can close (derivation in DESIGN.md 5j).
+        // The lane holding mu passes it whenever any lane does not fail, so a row with no failing lane
+        // never takes the (F, m) term.  Failing rows are flagged (viol) and re-run by spec2_kernel.
+        auto step2 = [&](uint32_t o1, uint32_t o2, float vp0, float vp1) {
+            if constexpr (L2) {
+                f2 e1, a1, pr, e2, a2;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+                asm("s_set_gpr_idx_on %[o], gpr_idx(SRC0)\n\t"
+                    "v_mov_b64 %[e], v[2:3]\n\t"
+                    "v_mov_b64 %[a], v[42:43]\n\t"
+                    "v_mov_b64 %[p], v[82:83]\n\t"
+                    "s_set_gpr_idx_off"
+                    : [e] "=&v"(e1), [a] "=&v"(a1), [p] "=&v"(pr)
+                    : [o] "s"(o1), "{v[2:33]}"(TA[0]), "{v[34:41]}"(TB[0]), "{v[42:73]}"(TA[1]), "{v[74:81]}"(TB[1]),
+                      "{v[82:113]}"(TA[2]), "{v[114:121]}"(TB[2])
+                    : "m0");
+                asm("s_set_gpr_idx_on %[o], gpr_idx(SRC0)\n\t"
+                    "v_mov_b64 %[e], v[2:3]\n\t"
+                    "v_mov_b64 %[a], v[42:43]\n\t"
+                    "s_set_gpr_idx_off"
+                    : [e] "=&v"(e2), [a] "=&v"(a2)
+                    : [o] "s"(o2), "{v[2:33]}"(TA[0]), "{v[34:41]}"(TB[0]), "{v[42:73]}"(TA[1]), "{v[74:81]}"(TB[1]),
+                      "{v[82:113]}"(TA[2]), "{v[114:121]}"(TB[2])
+                    : "m0");
+#pragma clang diagnostic pop
+                // heavy constants {A_S, A_F}, {X_SS, X_FF}, {X_SF} of s1 and s2 from the lane tables
+                const uint32_t u1 = o1 >> 1, u2 = o2 >> 1;
+                const f2 h1 = {readlane_f(cAS, u1), readlane_f(cAF, u1)}, x1 = {readlane_f(cXSS, u1), readlane_f(cXFF, u1)};
+                const f2 h2 = {readlane_f(cAS, u2), readlane_f(cAF, u2)}, x2 = {readlane_f(cXSS, u2), readlane_f(cXFF, u2)};
+                f2 s1 = {kInf, kInf}, s2 = {kInf, kInf};
+                if constexpr (SX) {
+                    s1.x = readlane_f(cXSF, u1);
+                    s2.x = readlane_f(cXSF, u2);
+                }
+                const float F = CF.y, c = CF.x;
+                const float pm = fminf(v[0], v[1]);  // the lane's minimum of the scores before the chunk
+                // light positions (slot 0: j - 1 is p0 - 1, the pred table; slot 1: j - 1 is slot 0)
+                const f2 cb = e2 + (f2){pr.x, e1.x};                  // fl(eb_j(s2) + eb_{j-1}(s1))
+                const f2 f1 = e2 + (f2){pr.y, a1.x};                  // fl(eb_j(s2) + ea_{j-1}(s1))
+                const f2 fx = a2 + (f2){x1.y, x1.y};                  // fl(ea_j(s2) + X_FF(s1))
+                const f2 fa = (f2){fminf(f1.x, fx.x), fminf(f1.y, fx.y)};
+                const f2 xa = fa + (f2){F, F};
+                const f2 xb = cb + (f2){vp0, vp1};
+                // F: the speculated (F, F) term and every other term of F's row
+                const float Fn = (x2.y + x1.y) + F;
+                const f2 qb = ((f2){h2.y, h2.y} + (f2){e1.x, e1.y}) + (f2){vp1, v[0]};  // (q, q-1): v_{q-1}
+                const f2 qa = ((f2){h2.y, h2.y} + a1) + (f2){F, F};                     // (q, F)
+                float nm = (x2.y + h1.y) + pm;                                          // (F, m)
+                nm = fminf(nm, fminf(fminf(qb.x, qb.y), fminf(qa.x, qa.y)));
+                // the margin bound of the light positions' (F, m) term
+                const float Rf = x1.y + F;
+                const float thr = Rf + (m.emax2 + Rf) * 0x1p-20f;
+                const float Lf = h1.y + pm;
+                asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+                             : "+v"(viol)
+                             : "v"(nm), "v"(Fn)
+                             : "vcc");
+                asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, 0, %0, vcc"
+                             : "+v"(viol)
+                             : "v"(Lf), "v"(thr)
+                             : "vcc");
+                // S (this lane's partial)
+                const f2 sb = ((f2){h2.x, h2.x} + (f2){e1.x, e1.y}) + (f2){vp1, v[0]};  // (q, q-1)
+                const f2 sa = ((f2){h2.x, h2.x} + a1) + (f2){F, F};                     // (q, F)
+                float cn = fminf((x2.x + x1.x) + c, (x2.x + h1.x) + pm);               // (S, S), (S, m)
+                cn = fminf(cn, fminf(fminf(sb.x, sb.y), fminf(sa.x, sa.y)));
+                if constexpr (SX) {
+                    cn = fminf(cn, (x2.x + s1.x) + F);   // (S, F)
+                    cn = fminf(cn, (s2.x + x1.y) + F);   // (F, F)
+                    cn = fminf(cn, (s2.x + h1.y) + pm);  // (F, m)
+                }
+                v[0] = fminf(xa.x, xb.x);
+                v[1] = fminf(xa.y, xb.y);
+                CF = (f2){cn, Fn};
+            }
+        };
+
         // ---- exchange state
         float* const ring_w = ring + w * kR * 64;
         const float* const ring_prev = ring_w - kR * 64;
@@ -868,6 +1119,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         const bool hpub = helped && w == 1;
         const bool hrd = kXh && w == (uint32_t)W - 2 && (g + 1) * W < m.nblk;
         float bprev = kInf;  // boundary score of observation t-1 for the next step (uniform)
+    float bprev2 = kInf;  // L2: ... of t-2 (a chunk's step reads the previous block's two last scores)
 
         auto give_up = [&]() -> bool { return ++spins > kSpinLimit; };
         // SVH_PIPE_XL: is workgroup og of this row on this wave's XCD?  (bounded poll of its id; not
@@ -972,11 +1224,21 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 if constexpr (DST == 2) {
                     if ((t & 63u) == 0) wait_cons((int)t - (int)kGR + 64);
                 }
-                step(o, ChainIn<-1>{bprev});
-                ring_put(t, v[SM - 1]);
-                if constexpr (DST == 2) put_gran1(t, readlane_f(v[SM - 1], 63));
+                if constexpr (L2) {
+                    // t odd: the chunk's first observation (nothing to compute; publish v_1 of the
+                    // state before it); t even: the chunk (publish v_0 of the state after it)
+                    if ((t & 1u) == 0) step2(sym1(t - 1), o, shr_in<0>(v[0], bprev2), shr_in<0>(v[1], bprev));
+                    const float pub = (t & 1u) ? v[1] : v[0];
+                    ring_put(t, pub);
+                    if constexpr (DST == 2) put_gran1(t, readlane_f(pub, 63));
+                } else {
+                    step(o, ChainIn<-1>{bprev});
+                    ring_put(t, v[SM - 1]);
+                    if constexpr (DST == 2) put_gran1(t, readlane_f(v[SM - 1], 63));
+                }
                 paths_after_rt(t);
                 if (t + 1 < len) {  // fetch the boundary score of t for the next step
+                    bprev2 = bprev;
                     if constexpr (SRC == 1) {
                         wait_prev(t + 1);
                         asm volatile("" ::: "memory");
@@ -997,9 +1259,10 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             if constexpr (SVH_PIPE_XL && SRC == 1 && kXh) {
                 if (hpub) cons_plain = xcc_local(g - 1);
             }
-            // publish the state at first-1 and fetch the boundary of first-1
-            ring_put(first - 1, v[SM - 1]);
-            if constexpr (DST == 2) put_gran1(first - 1, readlane_f(v[SM - 1], 63));
+            // publish the state at first-1 and fetch the boundary of first-1 (L2: first - 1 = 0 is
+            // even, the published score is v_0)
+            ring_put(first - 1, v[L2 ? 0 : SM - 1]);
+            if constexpr (DST == 2) put_gran1(first - 1, readlane_f(v[L2 ? 0 : SM - 1], 63));
             asm volatile("" ::: "memory");
             put_cnt(first);
             // initial progress (observations < first are done), published before the first wait:
@@ -1119,13 +1382,23 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                 }
                             }
                             if constexpr (SRC == 1) bv = bv_next;
-                            if constexpr (k == 0) {
+                            if constexpr (L2) {
+                                // groups start at odd t (tb = 1): k even is a chunk's first observation,
+                                // k odd its second, where the chunk runs with the previous block's
+                                // scores of t - 2 (lane k - 2 of bv; k = 1: lane 7 of the previous
+                                // group's) and t - 1 (lane k - 1)
+                                if constexpr (k & 1u) {
+                                    const uint32_t o1 = (uint32_t)((sw >> (8 * (k - 1))) & 0xFFu);
+                                    if constexpr (k == 1) step2(o1, o, shr_in<7>(v[0], bv_prev), shr_in<0>(v[1], bv));
+                                    else step2(o1, o, shr_in<(int)k - 2>(v[0], bv), shr_in<(int)k - 1>(v[1], bv));
+                                }
+                            } else if constexpr (k == 0) {
                                 step(o, ChainIn<7>{bv_prev});
                             } else {
                                 step(o, ChainIn<(int)k - 1>{bv});
                             }
                             if constexpr (SVH_PIPE_RING8) {  // kept for the group's two 16-byte stores
-                                gl[k] = v[SM - 1];
+                                gl[k] = L2 ? ((k & 1u) ? v[0] : v[1]) : v[SM - 1];
                                 if constexpr (k == 3 || k == 7)
                                     *reinterpret_cast<float4*>(ring_w + ring_idx(8 * j + k - 3, lane)) =
                                         make_float4(gl[k - 3], gl[k - 2], gl[k - 1], gl[k]);
@@ -1200,6 +1473,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 cw = load_window(cwi);
                 nw = load_window(cwi + 1);
                 bprev = readlane_f(bv_prev, 7);
+                bprev2 = readlane_f(bv_prev, 6);
                 if constexpr (SRC == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the prefetches
                 if constexpr (DST == 2) {
                     if (gpend_t && lane < 8)
@@ -1281,6 +1555,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
     if (tid == 0) {
         float cm = kInf, bvv = kInf;
         uint32_t bk = kNoRow, vi = 0;
+        bool rr = false;
         for (uint32_t u = 0; u < (uint32_t)W; ++u) {
             cm = fminf(cm, red[u * 4 + 0]);
             lex_min(bvv, bk, red[u * 4 + 1], __builtin_bit_cast(uint32_t, red[u * 4 + 2]));
@@ -1320,7 +1595,17 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             if (b.best) b.best[q] = bk2 == kNoRow ? -1 : (int64_t)bk2;
             x.viol[q] = vi;
             __hip_atomic_store(x.done + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rr = !PATHS && !L2 && m.rerun && vi;  // this workgroup re-runs the row (below)
         }
+        *tick = rr ? 1u : 0u;  // (the ticket itself is in id since the first barrier)
+    }
+    if constexpr (!PATHS && !L2) {
+        if (m.rerun) {
+            __syncthreads();
+            if (*tick == 1u) pipe_rerun_row<SM, W, SX>(m, b, q, lds);
+        }
+    }
+    if (tid == 0) {
         const uint32_t f = __hip_atomic_fetch_add(x.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (f == gridDim.x - 1) pipe_reset_counters(x);  // every workgroup has taken its ticket
     }

@@ -742,6 +742,18 @@ PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm, uint32_t waves, bool w
         c[7] = 0.0f;
         if (wide) wide_consts(o, c);
     }
+    // level 2 (pipe_kernel.h step2): every score >= 0 (the margin bound), the largest finite ea
+    bool nonneg = !wide;
+    for (float v : hm.val) nonneg = nonneg && v >= 0.0f;
+    for (float v : hm.emis) nonneg = nonneg && v >= 0.0f;
+    for (float v : hm.start) nonneg = nonneg && v >= 0.0f;
+    pp.emax2 = nonneg ? 0.0f : kInfH;
+    if (nonneg)
+        for (uint32_t p = 0; p < nL; ++p)
+            for (uint32_t o = 0; o < S; ++o) {
+                const float ea = hm.emis[(size_t)o * n + sh.light[p]] + sh.aw[0][p];
+                if (ea < kInfH) pp.emax2 = std::max(pp.emax2, ea);
+            }
     pp.ok = true;
     return pp;
 }
@@ -780,6 +792,8 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     view.G = p.G;
     view.sx = p.sx ? 1u : 0u;
     view.wide = p.wide ? 1u : 0u;
+    view.rerun = !p.wide && pipe_rerun_fits(p.P, p.W) ? 1u : 0u;
+    view.emax2 = p.emax2;
     // the pair-table step wherever it applies: TM = 4 (indexed operands, packed feeder terms:
     // 0.255 ms on the headline against 0.263 / 0.268 / 0.277 for TM 2 / 3 / 1 and 0.334 for the
     // per-slot tables); SVH_PIPE_TM selects another mode (A/B and tests: 0 per-slot
@@ -1150,6 +1164,11 @@ const DevicePipePlan* Model::pipe_paths_for(uint32_t nseq) const {
     return nullptr;
 }
 
+bool Model::pipe_l2_on() const {
+    return spec2_on && pipe.plan.ok && pipe_l2_supported(pipe.view) &&
+           (kernel_pref == SVH_KERNEL_AUTO || kernel_pref == SVH_KERNEL_PIPE);
+}
+
 const DevicePlan* Model::plan_for(bool paths) const {
     if (kernel_pref == SVH_KERNEL_GENERIC) return nullptr;
     const DevicePlan* p = paths ? paths_plan : &fast_plan;
@@ -1451,8 +1470,15 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
         i.pipe_waves = (int32_t)pipe.plan.W;
         i.pipe_groups = (int32_t)pipe.plan.G;
         i.pipe_max_nseq = kernel_pref == SVH_KERNEL_PIPE ? 0xFFFFFFFFu : pipe_max_nseq;
+        i.pipe_max_nseq_paths = kernel_pref == SVH_KERNEL_PIPE ? 0xFFFFFFFFu : pipe_max_nseq_paths;
     }
-    if (level == 2 && spec_level == 2 && spec2_on && nseq) {  // the chunks run on chip (spec2.hip)
+    if (level == 2 && spec_level == 2 && nseq && pipe_l2_on()) {  // the chunks on the pipelined plan
+        i.kernel = SVH_KERNEL_SPEC2_PIPE;
+        i.threads = (int32_t)(64 * pipe.plan.W);
+        i.slots = (int32_t)pipe.plan.SM;
+        i.lds_bytes = pipe_lds_bytes(pipe.plan.W, host.S);
+        i.spec_bytes = 0;
+    } else if (level == 2 && spec_level == 2 && spec2_on && nseq) {  // the chunks run on chip (spec2.hip)
         const Spec2Plan& sp = spec2.plan;
         i.kernel = SVH_KERNEL_SPEC2;
         i.threads = (int32_t)kSpec2Threads;
@@ -1488,9 +1514,12 @@ void Batch::init(uint32_t flags) {
     chain_paths = paths && model->band_for(true) != nullptr;
     if (paths && !chain_paths && model->host.n >= kNoPred)
         throw Error(SVH_E_UNSUPPORTED, "paths need states_num < 65535 for models the chain kernel does not cover");
+    timing = (flags & SVH_BATCH_NO_TIMING) == 0;
     DeviceGuard g(model->device);
-    hip_check(hipEventCreate(&ev_start), "hipEventCreate");
-    hip_check(hipEventCreate(&ev_stop), "hipEventCreate");
+    if (timing) {
+        hip_check(hipEventCreate(&ev_start), "hipEventCreate");
+        hip_check(hipEventCreate(&ev_stop), "hipEventCreate");
+    }
 }
 
 // (Re)load the batch's sequences: host packing, then asynchronous uploads on `s` into device
@@ -1729,6 +1758,7 @@ void Batch::run(uint32_t level, hipStream_t s) {
         fb.bp_off = p_bpoff;
     }
     pipe_ran = false;
+    l2_ran = false;
     if (const DevicePipePlan* pp = paths ? nullptr : model->pipe_for(nseq)) {  // pipelined plan: scratch
         pipe.ensure(nseq, pp->plan.G, s);
         pipe.note_launch(s);
@@ -1737,7 +1767,8 @@ void Batch::run(uint32_t level, hipStream_t s) {
     }
     auto launch_step_kernel = [&](const FusedBatch& b, bool want_paths) { model->launch_steps(b, want_paths, s); };
 
-    hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
+    last_stream = s;
+    if (timing) hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
     if (level <= 1 && pipe_paths) {
         // decoded paths on the pipelined plan: its path variant, the chain path variant for rows
         // whose speculation failed, the pipelined traceback (unflagged rows), the chain traceback
@@ -1762,9 +1793,14 @@ void Batch::run(uint32_t level, hipStream_t s) {
         FusedBatch cb = fb;  // chain buffers
         cb.run_mask = pipe.view.viol;
         hip_check(launch_chain(bpl->view, 1, cb, s), "chain Viterbi kernel (pipe paths fallback)");
-        // SVH_PIPE_SKIP_TRACEBACK=1: diagnostics only (timing of the forward kernels alone, e.g. of
-        // an ablation build whose path records are not stored; the paths read back are wrong)
+        // SVH_PIPE_SKIP_TRACEBACK=1: diagnostic builds only (-DSVH_PIPE_DIAG; timing of the forward
+        // kernels alone, e.g. of an ablation build whose path records are not stored; the paths read
+        // back are wrong).  The production library has no such knob.
+#ifdef SVH_PIPE_DIAG
         static const bool skip_tb = std::getenv("SVH_PIPE_SKIP_TRACEBACK") && std::atoi(std::getenv("SVH_PIPE_SKIP_TRACEBACK"));
+#else
+        constexpr bool skip_tb = false;
+#endif
         if (!skip_tb) {
             hip_check(launch_pipe_traceback(ppl->view, pb, p_pathoff, d_paths.as<int32_t>(),
                                             pipe.view.viol, s),
@@ -1785,14 +1821,19 @@ void Batch::run(uint32_t level, hipStream_t s) {
     } else {
         const uint32_t n = model->host.n;
         const bool on_chip = level == 2 && model->spec2_on;
-        const uint32_t ready = level | (on_chip ? 0x100u : 0u);
+        // level 2 on the pipelined latency plan (pipe_l2.hip): every chunk of every row in one
+        // launch into the second half of vbuf; rows whose speculation fails run again on spec2_kernel
+        // from the first step's state (first half) into the second half; the tail reads row nseq + q
+        const bool l2pipe = on_chip && model->pipe_l2_on();
+        const uint32_t ready = level | (on_chip ? 0x100u : 0u) | (l2pipe ? 0x200u : 0u);
         if (spec_ready_level != ready) {
             std::vector<uint32_t> nch(nseq), tb(nseq), vrow(nseq);
             for (uint32_t q = 0; q < nseq; ++q) {
                 nch[q] = (lens[q] - 1) / level;
                 tb[q] = 1 + nch[q] * level;
-                vrow[q] = on_chip ? q : (nch[q] & 1u) * nseq + q;  // the row the chunks end in
+                vrow[q] = l2pipe ? nseq + q : on_chip ? q : (nch[q] & 1u) * nseq + q;  // the row the chunks end in
             }
+            if (l2pipe) d_l2viol.alloc((size_t)nseq * 4);
             d_nchunks.upload(nch.data(), nch.size() * 4, s);
             d_tbegin.upload(tb.data(), tb.size() * 4, s);
             d_vrow.upload(vrow.data(), vrow.size() * 4, s);
@@ -1804,6 +1845,19 @@ void Batch::run(uint32_t level, hipStream_t s) {
         }
         float* vb = d_vbuf.as<float>();
         hip_check(launch_first_step(csr, fb.symbols, fb.sym_off, nseq, vb, s), "spec first step");
+        if (l2pipe) {
+            const DevicePipePlan& pl = model->pipe;
+            pipe.ensure(nseq, pl.plan.G, s);
+            pipe.note_launch(s);
+            PipeScratch x2 = pipe.view;
+            x2.viol = d_l2viol.as<uint32_t>();  // its own flags: the tail's pass rewrites pipe.view.viol
+            FusedBatch lb = fb;
+            lb.scores = vb + (size_t)nseq * n;
+            lb.best = nullptr;
+            lb.pipe = nullptr;
+            hip_check(launch_pipe_l2(pl.view, lb, x2, s), "pipelined level-2 kernel");
+            l2_ran = true;
+        }
         if (on_chip) {  // every chunk of every sequence in one launch, v in place (row q)
             Spec2Batch sb;
             sb.symbols = fb.symbols;
@@ -1812,6 +1866,10 @@ void Batch::run(uint32_t level, hipStream_t s) {
             sb.nchunks = d_nchunks.as<uint32_t>();
             sb.v = vb;
             sb.nseq = nseq;
+            if (l2pipe) {  // only the rows the pipelined pass flagged, into the second half
+                sb.run_mask = d_l2viol.as<uint32_t>();
+                sb.v_out = vb + (size_t)nseq * n;
+            }
             hip_check(launch_spec2(model->spec2.view, sb, s), "spec2 kernel");
             if (model->spec2.view.stamps) {
                 hip_check(hipStreamSynchronize(s), "spec2 stamps");
@@ -1839,7 +1897,7 @@ void Batch::run(uint32_t level, hipStream_t s) {
         tail.bp_off = nullptr;
         launch_step_kernel(tail, false);
     }
-    hip_check(hipEventRecord(ev_stop, s), "hipEventRecord");
+    if (timing) hip_check(hipEventRecord(ev_stop, s), "hipEventRecord");
     ran = true;
 }
 
@@ -2082,11 +2140,12 @@ void Batch::run_time_parallel(uint32_t seg, uint32_t probe, float tol, hipStream
         });
     }
     d_arena.reserve(arena.size());
-    hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
+    last_stream = s;
+    if (timing) hip_check(hipEventRecord(ev_start, s), "hipEventRecord");
     hip_check(hipMemcpyAsync(d_arena.ptr, arena.data(), arena.size(), hipMemcpyHostToDevice, s), "time-parallel rows");
     const uint8_t* const base = d_arena.as<uint8_t>();
     for (auto& op : ops) op(base);
-    hip_check(hipEventRecord(ev_stop, s), "hipEventRecord");
+    if (timing) hip_check(hipEventRecord(ev_stop, s), "hipEventRecord");
     std::vector<uint32_t> flags(nflags);
     if (nflags)
         hip_check(hipMemcpyAsync(flags.data(), d_flag.ptr, (size_t)nflags * 4, hipMemcpyDeviceToHost, s), "flags D2H");
@@ -2169,11 +2228,16 @@ void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) co
             hip_check(hipStreamSynchronize(s), "stamps");
             ppl->report_stamps(b.nseq);
         }
-        // rows whose speculation failed run again on the serial chain kernel (the others exit);
-        // SVH_PIPE_SKIP_FALLBACK=1: diagnostics only (timing without the second launch; results of
-        // flagged rows would be wrong)
+        // rows whose speculation failed: the latency plan re-runs them itself (PipeModel::rerun:
+        // no second launch on the common path); otherwise they run again on the serial chain
+        // kernel (the others exit);
+        // SVH_PIPE_SKIP_FALLBACK=1: diagnostic builds only (-DSVH_PIPE_DIAG; timing without the
+        // second launch; results of flagged rows would be wrong)
+#ifdef SVH_PIPE_DIAG
         static const bool skip_fb = std::getenv("SVH_PIPE_SKIP_FALLBACK") && std::atoi(std::getenv("SVH_PIPE_SKIP_FALLBACK"));
         if (skip_fb) return;
+#endif
+        if (!ppl->plan.wide && ppl->view.rerun) return;
         FusedBatch fb = b;
         fb.run_mask = b.pipe->viol;
         fb.pipe = nullptr;
@@ -2227,18 +2291,22 @@ void Batch::inject_fault(hipStream_t s) {
 uint64_t Batch::pipe_fallbacks() {
     DeviceGuard g(model->device);
     if (!ran) throw Error(SVH_E_STATE, "no run recorded");
-    if (!pipe_ran) return 0;
-    hip_check(hipEventSynchronize(ev_stop), "hipEventSynchronize");
-    std::vector<uint32_t> v(nseq);
-    hip_check(hipMemcpy(v.data(), pipe.view.viol, (size_t)nseq * 4, hipMemcpyDeviceToHost), "fallback flags D2H");
+    if (!pipe_ran && !l2_ran) return 0;
+    if (timing) hip_check(hipEventSynchronize(ev_stop), "hipEventSynchronize");
+    else hip_check(hipStreamSynchronize(last_stream), "hipStreamSynchronize");
+    std::vector<uint32_t> v(nseq, 0), v2(nseq, 0);
+    if (pipe_ran) hip_check(hipMemcpy(v.data(), pipe.view.viol, (size_t)nseq * 4, hipMemcpyDeviceToHost), "fallback flags D2H");
+    // level 2 on the pipelined plan: its rows re-run by spec2_kernel count too
+    if (l2_ran) hip_check(hipMemcpy(v2.data(), d_l2viol.ptr, (size_t)nseq * 4, hipMemcpyDeviceToHost), "fallback flags D2H");
     uint64_t c = 0;
-    for (uint32_t x : v) c += x != 0;
+    for (uint32_t q = 0; q < nseq; ++q) c += (v[q] | v2[q]) != 0;
     return c;
 }
 
 float Batch::elapsed_ms() {
     DeviceGuard g(model->device);
     if (!ran) throw Error(SVH_E_STATE, "no run recorded");
+    if (!timing) throw Error(SVH_E_STATE, "batch created with SVH_BATCH_NO_TIMING: no run events");
     hip_check(hipEventSynchronize(ev_stop), "hipEventSynchronize");
     float ms = 0;
     hip_check(hipEventElapsedTime(&ms, ev_start, ev_stop), "hipEventElapsedTime");

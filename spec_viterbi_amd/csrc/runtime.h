@@ -139,6 +139,9 @@ struct PipePlan {
     std::vector<uint32_t> lrow; // [P]
     std::vector<float> hc;      // [S][8]
     bool wide = false;          // pipe_wide.hip layout: tab [nblk][S][SM/2][64][4], W sequences per workgroup
+    // _spec level 2 on this plan (pipe_l2.hip): the largest finite ea = fl(E_o[p] + aw_p), or +inf
+    // when some score is negative (its margin check needs every score >= 0) or the plan is wide
+    float emax2 = 0.0f;
     // decoded paths (PipeModel::pflags / spos / hx_exist / hl_exist / ties_heavy)
     std::vector<uint8_t> pflags;  // [P]
     std::vector<int32_t> spos;    // [n]
@@ -238,6 +241,9 @@ struct Model {
     // _spec level 2 on chip (spec2.hip): built by spec_build(2) unless SVH_SPEC_DENSE=1
     DeviceSpec2Plan spec2;
     bool spec2_on = false;
+    // level 2 runs on the pipelined latency plan (pipe_l2.hip) with spec2_kernel as its exact
+    // fallback: the model has both, every score >= 0, and the kernel preference allows the pipe
+    bool pipe_l2_on() const;
     bool spec_dense = false;  // svh_model_opts.flags & SVH_MODEL_SPEC_DENSE
 
     Model(const HostModel& h, const svh_model_opts* opts);
@@ -292,9 +298,16 @@ struct Batch {
 
     // _spec runs
     DeviceBuffer d_vbuf, d_nchunks, d_tbegin, d_vrow;
+    DeviceBuffer d_l2viol;  // level 2 on the pipelined plan: rows whose speculation failed (spec2 re-runs them)
+    bool l2_ran = false;    // the last run used it
     uint32_t spec_ready_level = 0;
     uint32_t max_chunks = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    // SVH_BATCH_NO_TIMING: run() records no start / stop events (each event record is a marker on
+    // the stream that the next kernel waits behind: ~3 us per record on MI355X); elapsed_ms() is then
+    // unavailable and pipe_fallbacks() waits on the last run's stream instead
+    bool timing = true;
+    hipStream_t last_stream = nullptr;
     bool ran = false;
 
     // host tables of the last load (copied into h_in)

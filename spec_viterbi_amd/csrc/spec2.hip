@@ -90,6 +90,7 @@ __global__ __launch_bounds__(kS2Threads) void spec2_kernel(Spec2Model m, Spec2Ba
     const uint32_t n = m.n, H = m.H, nhs = m.nhs;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint32_t q = blockIdx.x;
+    if (b.run_mask && b.run_mask[q] == 0) return;  // a fallback pass: only the flagged rows
     const Spec2Lds L = spec2_lds_layout(n, KL, m.NP, H);
     float* vl = lds + L.v;                                       // [n + 1]: vl[n] = +inf
     float2* PR = reinterpret_cast<float2*>(lds + L.pairs);       // LP [n][KL] | CP [NP]
@@ -353,7 +354,8 @@ __global__ __launch_bounds__(kS2Threads) void spec2_kernel(Spec2Model m, Spec2Ba
 #endif
     for (uint32_t h = t; h < H; h += kS2Threads) vl[m.hrow[h]] = okey_val(hacc[h]);
     __syncthreads();
-    for (uint32_t j = t; j < n; j += kS2Threads) vg[j] = vl[j];
+    float* vo = b.v_out ? b.v_out + (size_t)q * n : vg;
+    for (uint32_t j = t; j < n; j += kS2Threads) vo[j] = vl[j];
 }
 
 template <int R, int KL, int NHS>

@@ -85,8 +85,8 @@ class DeviceModel:
     def spec_build(self, level: int, stream: int | None = None) -> None:
         _lib.check(_lib.lib.svh_spec_build(self._h, int(level), ctypes.c_void_p(stream or 0)))
 
-    def batch(self, seqs, paths: bool = False) -> "DeviceBatch":
-        return DeviceBatch(self, seqs, paths)
+    def batch(self, seqs, paths: bool = False, timing: bool = True) -> "DeviceBatch":
+        return DeviceBatch(self, seqs, paths, timing)
 
     def viterbi(self, seqs, level: int = 0, paths: bool = False):
         """One-shot: scores [nseq, n] (+ best state [nseq], + paths list if requested).
@@ -154,7 +154,9 @@ class DeviceModel:
 class DeviceBatch:
     """Sequences resident in HBM; run() enqueues one pass on a HIP stream (svh_batch_*)."""
 
-    def __init__(self, model: DeviceModel, seqs, paths: bool = False):
+    def __init__(self, model: DeviceModel, seqs, paths: bool = False, timing: bool = True):
+        """timing=False: run() records no start/stop events on the stream (SVH_BATCH_NO_TIMING;
+        elapsed_ms() then raises) -- for callers that time the stream themselves."""
         self.model = model
         self.offsets, symbols = pack_sequences(seqs)
         self.nseq = self.offsets.size - 1
@@ -162,7 +164,8 @@ class DeviceBatch:
         self.total = int(self.offsets[-1])
         h = ctypes.c_void_p()
         _lib.check(_lib.lib.svh_batch_create(model.handle, self.nseq, _p(self.offsets, _u64), _p(symbols, _u64),
-                                             _lib.SVH_BATCH_PATHS if paths else 0, ctypes.byref(h)))
+                                             (_lib.SVH_BATCH_PATHS if paths else 0) |
+                                             (0 if timing else _lib.SVH_BATCH_NO_TIMING), ctypes.byref(h)))
         self._h = h
 
     def run(self, level: int = 0, stream: int | None = None) -> None:

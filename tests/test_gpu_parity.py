@@ -173,17 +173,24 @@ def test_errors():
 
 
 def test_spec2_plan_reported():
-    """svh_batch_plan at level 2 names the on-chip chunk kernel (SVH_KERNEL_SPEC2) with its
-    workgroup size, LDS and table bytes; level 0 of the same batch keeps the step kernel."""
+    """svh_batch_plan at level 2: an MSV-shaped model under AUTO runs the chunks on the pipelined
+    latency plan (SVH_KERNEL_SPEC2_PIPE: 256 threads, 2 slots, nothing precomputed); with another
+    kernel preference the on-chip chunk kernel (SVH_KERNEL_SPEC2) with its workgroup size, LDS and
+    table bytes; level 0 of the same batch keeps the step kernel."""
     hmm = svh.read_HMM(chmm("100.chmm"))
     seqs = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
     model = svh.DeviceModel(hmm)
     model.spec_build(2)
     batch = model.batch(seqs)
     p2, p0 = batch.plan(2), batch.plan(0)
+    assert p2["kernel"] == _lib.SVH_KERNEL_SPEC2_PIPE and p2["threads"] == 256 and p2["slots"] == 2
+    assert p2["spec_bytes"] == 0 and p2["spec_level"] == 2
+    assert p0["kernel"] not in (_lib.SVH_KERNEL_SPEC2, _lib.SVH_KERNEL_SPEC2_PIPE)
+    model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_GENERIC)
+    model.spec_build(2)
+    p2 = model.batch(seqs).plan(2)
     assert p2["kernel"] == _lib.SVH_KERNEL_SPEC2 and p2["threads"] == 1024
     assert p2["lds_bytes"] > 0 and p2["spec_bytes"] > 0 and p2["spec_level"] == 2
-    assert p0["kernel"] != _lib.SVH_KERNEL_SPEC2
 
 
 def test_batch_api_device_resident_rerun():

@@ -97,6 +97,44 @@ def test_pipe_auto_selects_pipe_for_small_batches():
     assert chain.plan()["kernel"] == _lib.SVH_KERNEL_CHAIN
 
 
+@pytest.mark.parametrize("name,ess_name,nseq", [("2405.chmm", "emit_50_3500_20.ess", 100),
+                                                 ("1001.chmm", "emit_3_3500_20.ess", 200),
+                                                 ("100.chmm", "emit_3_3500_20.ess", 400)])
+def test_pipe_auto_two_workgroups_per_cu(name, ess_name, nseq):
+    """AUTO's latency plan past one workgroup per CU (runtime.cpp: pipe_max_nseq = 2 x CUs / G for
+    scores-only batches): 100 sequences of 2405.chmm (G = 5, 500 workgroups), 200 of 1001.chmm
+    (G = 2, 400) and 400 of 100.chmm (G = 1, 400) on 256 CUs.  Rows are the reference file's
+    sequences and rotated copies of them (np.roll: the same symbol statistics, so the speculation
+    holds as on the file); every row bit-exact against the oracle (the file rows of 2405 also
+    against the committed digests), best states equal, no row fell back."""
+    import hashlib
+
+    hmm = svh.read_HMM(chmm(name))
+    base = svh.read_emit_seq(ess(ess_name))
+    seqs = [base[q % len(base)] if q < len(base) else np.roll(base[q % len(base)], 97 * (q // len(base)))
+            for q in range(nseq)]
+    if name == "100.chmm":  # 400 x 3500 x 101 states through the oracle: shorter rows keep it quick
+        seqs = [s[: 1200 + 7 * q] for q, s in enumerate(seqs)]
+    model = svh.DeviceModel(hmm)
+    info = model.info()
+    G = info["pipe_groups"]
+    assert info["pipe_max_nseq"] == 2 * info["cu_count"] // G, info
+    assert info["cu_count"] < nseq * G <= 2 * info["cu_count"], (nseq, G, info["cu_count"])
+    batch = model.batch(seqs)
+    assert batch.plan()["kernel"] == _lib.SVH_KERNEL_PIPE
+    batch.run()
+    s, b = batch.read()
+    assert batch.fallbacks() == 0
+    oracle_check(hmm, seqs, s, b)
+    if name == "2405.chmm":
+        rows = load_digests()[f"{name} x {ess_name}"]
+        for q in range(len(base)):
+            assert hashlib.sha256(np.ascontiguousarray(s[q]).tobytes()).hexdigest() == rows[q]["scores_sha256"], q
+            assert b[q] == rows[q]["best_state"], q
+    batch.close()
+    model.close()
+
+
 @pipes
 @pytest.mark.parametrize("name", ["100.chmm", "500.chmm", "1001.chmm", "1509.chmm", "2050.chmm"])
 def test_pipe_reference_models_vs_oracle(name, kern):
@@ -151,10 +189,12 @@ def test_pipe_long_sequence_many_ring_laps(kern):
 @pipes
 def test_pipe_fallback_rows_match_oracle(kern):
     """Models whose feeder row takes its light term (cheap M -> N): the speculation fails, those
-    rows are re-run serially, and every score still matches the oracle."""
+    rows are re-run serially, and every score still matches the oracle.  The latency plan re-runs
+    them inside the pass (pipe_rerun_row, by the row's combining workgroup: one workgroup per row at
+    300 states, the last of two at 700), the wide plan on the serial chain kernel."""
     total_fb = 0
-    for seed in range(6):
-        hmm = random_chain_hmm(300, S=8, seed=seed)
+    for seed in range(8):
+        hmm = random_chain_hmm(300 if seed < 6 else 700, S=8, seed=seed)
         # make M_j -> N nearly free so N's light term wins somewhere
         rows, cols = hmm.trans_rows.astype(np.int64), hmm.trans_cols.astype(np.int64)
         probs = hmm.trans_probs.copy()

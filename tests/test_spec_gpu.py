@@ -105,29 +105,60 @@ def _neg_hmm(seed):
     return hmm
 
 
+def _near_tie_hmm(seed):
+    """Heavy rows (degree ~600) whose candidate terms sit 0..17 ulps apart: every score is
+    3 * (1 + k 2^-23) with k drawn from {0, 1, 2, 15, 16, 17}, so the sums c_m = fl(b_m + v_m) of a
+    heavy row's terms crowd around its minimum within the on-chip kernel's 16-ulp pruning margin
+    (spec2.hip theta_of).  Pins the pruning bound bit-exactly against the oracle where it is
+    tightest."""
+    hmm = random_hmm(600, S=6, out_degree=3, dense_rows=(0, 3, 9), seed=seed)
+    rng = np.random.default_rng(seed)
+    ks = np.array([0, 1, 2, 15, 16, 17], np.float64)
+
+    def near(shape):
+        return (3.0 * (1.0 + rng.choice(ks, size=shape) * 2.0 ** -23)).astype(np.float32)
+
+    tp = hmm.trans_probs.copy()
+    fin = np.isfinite(tp)
+    tp[fin] = near(int(fin.sum()))
+    hmm.trans_probs = tp
+    em = hmm.emissions.copy()
+    fin = np.isfinite(em)
+    em[fin] = near(int(fin.sum()))
+    hmm.emissions = em
+    return hmm
+
+
 SPEC2_MODELS = {
     "chmm_gen": lambda: random_hmm(900, S=10, out_degree=3, seed=21),                # heavy rows of degree 5..10
     "dense_rows": lambda: random_hmm(257, out_degree=2, dense_rows=(5, 100), seed=22, zero_emis=0.05),
     "chain_ties": lambda: random_chain_hmm(700, S=8, seed=23, ties=True),            # exact ties everywhere
     "chain_inf": lambda: random_chain_hmm(1300, S=8, seed=24, inf_edges=0.2, zero_emis=0.1, feed_c=True),
-    "chain_gap": lambda: random_chain_hmm(2600, S=4, seed=25, gap=1000, start=(0, 5)),  # R = 4 rows per thread
+    "chain_gap": lambda: random_chain_hmm(2600, S=4, seed=25, gap=1000, start=(0, 5)),  # n = 2602: R = 3 rows per thread
+    "chain_r4": lambda: random_chain_hmm(3600, S=4, seed=28, gap=1700, start=(0, 9)),  # n = 3602: R = 4 rows per thread
+    "near_ties": lambda: _near_tie_hmm(29),                                          # candidates 0..17 ulps apart
     "negative": lambda: _neg_hmm(26),                                                # pruning off
     "one_state": lambda: random_hmm(1, out_degree=1, seed=27),
 }
 
 
+@pytest.mark.parametrize("pref", ["auto", "spec2"])
 @pytest.mark.parametrize("name", list(SPEC2_MODELS))
-def test_spec2_on_chip_vs_oracle(name):
-    """_spec level 2 evaluated on chip from the folded sparse matrices (spec2.hip, no dense
-    products) against the oracle's product-based GraphBLAS_spec_impl restatement, bit-exact, on
-    ragged sequences (chunks + a tail of 0 or 1 observations, lengths 1 and 2 included); the same
-    batch on the dense-product path (SVH_MODEL_SPEC_DENSE) must agree bit for bit too."""
+def test_spec2_on_chip_vs_oracle(name, pref):
+    """_spec level 2 evaluated on chip from the folded sparse matrices (no dense products) against
+    the oracle's product-based GraphBLAS_spec_impl restatement, bit-exact, on ragged sequences
+    (chunks + a tail of 0 or 1 observations, lengths 1 and 2 included): under AUTO (the MSV-shaped
+    models run the chunks on the pipelined plan, pipe_l2.hip, with spec2_kernel re-running the rows
+    it flags) and with spec2_kernel for every row (another kernel preference); the same batch on the
+    dense-product path (SVH_MODEL_SPEC_DENSE) must agree bit for bit too."""
     hmm = SPEC2_MODELS[name]()
     S = int(hmm.emit_num)
     seqs = random_seqs(S, [1, 2, 3, 4, 5, 64, 257, 1000, 1501], seed=sum(map(ord, name)))
-    model = svh.DeviceModel(hmm)
+    model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_AUTO if pref == "auto" else _lib.SVH_KERNEL_GENERIC)
     model.spec_build(2)
     assert model.info()["spec_bytes"] == 0, "expected the on-chip level-2 kernel (no products)"
+    if pref == "spec2":
+        assert model.batch(seqs[:1]).plan(2)["kernel"] == _lib.SVH_KERNEL_SPEC2
     got, best = model.viterbi(seqs, level=2)
     refs = oracle.viterbi_spec_batch(hmm, 2, seqs)  # the products built once
     for q, seq in enumerate(seqs):
@@ -142,6 +173,57 @@ def test_spec2_on_chip_vs_oracle(name):
         got2, _ = dense.viterbi(seqs, level=2)
         for q in range(len(seqs)):
             assert bit_equal(got[q], got2[q]), (name, q, first_mismatch(got[q], got2[q]))
+
+
+def test_spec2_pipe_headline_no_fallback():
+    """BASELINE config 4 at level 2 on the pipelined latency plan (pipe_l2.hip, SVH_KERNEL_SPEC2_PIPE):
+    every chunk of the 50 rows in one launch (5 workgroups per row), the one-observation tails on
+    the step kernel; all 50 rows against the oracle's level-2 digests and no row handed to
+    spec2_kernel (the speculated (F, m) terms and F's light terms never win on the reference data,
+    so a fallback would hide a wrong pipelined row)."""
+    import hashlib
+
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
+    model = svh.DeviceModel(hmm)
+    model.spec_build(2)
+    batch = model.batch(seqs)
+    assert batch.plan(2)["kernel"] == _lib.SVH_KERNEL_SPEC2_PIPE
+    for _ in range(2):  # a re-run of the same batch (scratch epochs, the flags of the last run)
+        batch.run(2)
+        got, best = batch.read()
+        assert batch.fallbacks() == 0
+        rows = load_digests()["2405.chmm x emit_50_3500_20.ess level 2"]
+        bad = [q for q in range(50)
+               if hashlib.sha256(np.ascontiguousarray(got[q], np.float32).tobytes()).hexdigest() != rows[q]["scores_sha256"]]
+        assert not bad, bad
+        assert np.array_equal(best, np.argmin(got, axis=1))
+
+
+@pytest.mark.parametrize("n_states", [300, 1300])
+def test_spec2_pipe_fallback_rows_match_oracle(n_states):
+    """Models whose feeder row takes its light term (M -> N free): the pipelined level-2 pass flags
+    those rows and spec2_kernel re-runs them from the first observation's state; every row still
+    equals the oracle's level 2 bit for bit, and rows did fall back."""
+    total = 0
+    for seed in range(3):
+        hmm = random_chain_hmm(n_states, S=8, seed=seed)
+        rows, cols = hmm.trans_rows.astype(np.int64), hmm.trans_cols.astype(np.int64)
+        probs = hmm.trans_probs.copy()
+        probs[(cols == 0) & (rows != 0)] = np.float32(0.0)
+        hmm.trans_probs = probs
+        seqs = random_seqs(8, [700, 1, 2, 40, 333, 64], seed=seed)
+        model = svh.DeviceModel(hmm)
+        model.spec_build(2)
+        batch = model.batch(seqs)
+        assert batch.plan(2)["kernel"] == _lib.SVH_KERNEL_SPEC2_PIPE
+        batch.run(2)
+        got, _ = batch.read()
+        total += batch.fallbacks()
+        refs = oracle.viterbi_spec_batch(hmm, 2, seqs)
+        for q in range(len(seqs)):
+            assert bit_equal(got[q], refs[q]), (seed, q, first_mismatch(got[q], refs[q]))
+    assert total > 0
 
 
 def test_spec2_large_model_takes_dense_path():
