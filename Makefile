@@ -20,12 +20,12 @@ HIP_SRCS  := $(wildcard $(CSRC)/fused_*.hip) $(CSRC)/misc.hip $(CSRC)/band.hip $
              $(CSRC)/pipe_tm1.hip $(CSRC)/pipe_tm1p.hip $(CSRC)/pipe_wide.hip $(CSRC)/pipe_wide_paths.hip $(CSRC)/pipe_paths.hip \
              $(CSRC)/spec2.hip $(CSRC)/pipe_l2.hip
 HOST_SRCS := $(CSRC)/runtime.cpp $(CSRC)/svh_api.cpp $(CSRC)/HIP_impl.cpp $(CSRC)/data_reader.cpp $(CSRC)/stream.cpp \
-             $(CSRC)/seqreader.cpp
+             $(CSRC)/seqreader.cpp $(CSRC)/chunker.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS))
 HDRS := $(wildcard $(CSRC)/*.h) $(wildcard include/*.h)
 
 CPP_TESTS := tests/cpp/test_HIP_impl tests/cpp/test_HIP_spec_impl tests/cpp/test_semantic_equality \
-             tests/cpp/test_readers_asan
+             tests/cpp/test_readers_asan tests/cpp/test_host_asan
 
 .PHONY: all lib oracle ref tests tools clean
 all: lib oracle tests tools ref
@@ -67,6 +67,20 @@ tests/cpp/test_readers_asan: tests/cpp/test_readers_asan.cpp $(CSRC)/data_reader
 		$(CSRC)/seqreader.h $(CSRC)/error.h include/data_reader.h include/HMM.h
 	$(CXX) -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -Iinclude -I$(CSRC) \
 		-o $@ tests/cpp/test_readers_asan.cpp $(CSRC)/data_reader.cpp $(CSRC)/seqreader.cpp
+
+# The rest of the host code under AddressSanitizer + UBSan (host side only: -fno-gpu-sanitize): the
+# host CSR and every plan builder of runtime.cpp and the file decoder's chunk hand-off
+# (chunker.cpp), linked with the uninstrumented kernel objects; the test touches no GPU.
+ASAN_HOST := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-gpu-sanitize
+ASAN_OBJS := $(patsubst $(CSRC)/%.cpp,$(BUILD)/asan/%.o,$(HOST_SRCS))
+$(BUILD)/asan/%.o: $(CSRC)/%.cpp $(HDRS) | $(BUILD)
+	mkdir -p $(BUILD)/asan
+	$(HIPCC) $(HOSTFLAGS) $(ASAN_HOST) -c $< -o $@
+$(BUILD)/asan/test_host_asan.o: tests/cpp/test_host_asan.cpp $(HDRS) | $(BUILD)
+	mkdir -p $(BUILD)/asan
+	$(HIPCC) $(HOSTFLAGS) $(ASAN_HOST) -c $< -o $@
+tests/cpp/test_host_asan: $(BUILD)/asan/test_host_asan.o $(ASAN_OBJS) $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIP_SRCS))
+	$(HIPCC) --offload-arch=$(ARCH) $(ASAN_HOST) -o $@ $^
 
 # The reference benchmark harness's per-sequence call loop over HIP_impl / HIP_spec_impl.
 tools/bench_harness: tools/bench_harness.cpp $(LIB) include/HIP_impl.h include/HIP_spec_impl.h

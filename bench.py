@@ -589,6 +589,8 @@ def main(argv=None):
         # its bound; on chip (spec2) the tables are read once per XCD like the step kernels'
         if spec2:
             ess_b = spec2_essential_bytes(n, int(info["S"]), lengths, int(plan["spec_bytes"]))
+        elif l2pipe:  # the level-0 plan's tables, read once per XCD, and nothing precomputed
+            ess_b = essential_bytes_per_launch(n, int(info["S"]), lengths, False)
         else:
             ess_b = algo if args.level >= 2 else essential_bytes_per_launch(n, int(info["S"]), lengths, args.paths)
         rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc, ess_b)

@@ -14,6 +14,7 @@
 #include <mutex>
 #include <thread>
 
+#include "chunker.h"
 #include "svh.h"
 
 namespace svh {
@@ -22,57 +23,6 @@ namespace svh {
 // Pipelined decoder
 // ---------------------------------------------------------------------------------------------
 namespace {
-
-struct Chunk {
-    std::vector<uint64_t> offsets;
-    std::vector<uint8_t> symbols;
-    uint64_t first = 0;
-};
-
-// Bounded hand-off from the parser thread; an exception or the end closes it.
-class ChunkQueue {
-  public:
-    explicit ChunkQueue(size_t cap) : cap_(cap) {}
-    bool push(Chunk&& c) {  // false: the consumer stopped
-        std::unique_lock<std::mutex> l(mu_);
-        cv_.wait(l, [&] { return q_.size() < cap_ || stop_; });
-        if (stop_) return false;
-        q_.push_back(std::move(c));
-        cv_.notify_all();
-        return true;
-    }
-    void close(std::exception_ptr e) {
-        std::lock_guard<std::mutex> l(mu_);
-        closed_ = true;
-        err_ = e;
-        cv_.notify_all();
-    }
-    bool pop(Chunk& c) {  // false at the end (rethrows the producer's error)
-        std::unique_lock<std::mutex> l(mu_);
-        cv_.wait(l, [&] { return !q_.empty() || closed_; });
-        if (!q_.empty()) {
-            c = std::move(q_.front());
-            q_.pop_front();
-            cv_.notify_all();
-            return true;
-        }
-        if (err_) std::rethrow_exception(err_);
-        return false;
-    }
-    void stop() {
-        std::lock_guard<std::mutex> l(mu_);
-        stop_ = true;
-        cv_.notify_all();
-    }
-
-  private:
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::deque<Chunk> q_;
-    size_t cap_;
-    bool closed_ = false, stop_ = false;
-    std::exception_ptr err_;
-};
 
 struct Slot {
     std::unique_ptr<Batch> batch;
@@ -93,21 +43,7 @@ uint64_t decode_file(Model* model, const std::string& path, int format, uint32_t
     auto reader = std::make_shared<SeqReader>(path, format);  // opens (errors surface here)
 
     ChunkQueue queue(2);
-    std::thread producer([&queue, reader, max_seqs, max_symbols] {
-        try {
-            uint64_t first = 0;
-            while (true) {
-                Chunk c;
-                if (!reader->next(max_seqs, max_symbols, c.offsets, c.symbols)) break;
-                c.first = first;
-                first += c.offsets.size() - 1;
-                if (!queue.push(std::move(c))) break;
-            }
-            queue.close(nullptr);
-        } catch (...) {
-            queue.close(std::current_exception());
-        }
-    });
+    std::thread producer([&queue, reader, max_seqs, max_symbols] { produce_chunks(*reader, queue, max_seqs, max_symbols); });
 
     DeviceGuard g(model->device);
     hipStream_t xs = nullptr;
