@@ -594,6 +594,21 @@ def main(argv=None):
         else:
             ess_b = algo if args.level >= 2 else essential_bytes_per_launch(n, int(info["S"]), lengths, args.paths)
         rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc, ess_b)
+        if plan["kernel"] == 5 and not args.paths and args.level <= 1 and batch:
+            # the latency plan's own floor, measured live: the same launch with every boundary exchange
+            # removed (svh_batch_step_floor_ms: each wave sweeps its block with no neighbour input and no
+            # waits), i.e. the step's per-observation issue time at one wave per SIMD plus the prologue
+            floor_ms = batch.step_floor_ms(10, sptr)
+            maxlen = max(lengths)
+            rl["latency_frac"] = round(floor_ms / kernel_ms, 4)
+            rl["latency"] = {"step_floor_ms": round(floor_ms, 4), "frac": rl["latency_frac"],
+                             "floor_ns_per_observation": round(floor_ms * 1e6 / maxlen, 2),
+                             "kernel_ns_per_observation": round(kernel_ms * 1e6 / maxlen, 2),
+                             "exchange_and_fill_ms": round(kernel_ms - floor_ms, 4),
+                             "note": "step_floor = the same pipelined launch with every boundary exchange removed "
+                                     "(pipe_kernel.h FLOOR; DESIGN.md 5k); frac = floor / kernel_ms: the share of the "
+                                     "pass that is the step itself at one wave per SIMD; the rest is the exchange "
+                                     "(instructions, waits) and the fill of the 19-wave chain"}
         workload = (f"{args.model} x {ess_name}" +
                     (f" x{args.replicate} (file sequences + same-shape synthetic copies)" if args.replicate > 1 else "") +
                     (", LPT-sharded (strong scaling)" if strong else "") + ", " +

@@ -1,10 +1,13 @@
 // MI355X (gfx950) backend for the reference's Viterbi_spec_impl interface.
 //
 // Drops in beside GraphBLAS_spec_impl (reference: Viterbi_impl/GraphBLAS_spec_impl.h:8-30,
-// implementation GraphBLAS_spec_impl.cpp).  spec_with(hmm) uploads the model and, for
-// level >= 2, precomputes the emit_num^level products of level consecutive observations in HBM
-// (GraphBLAS_spec_impl.cpp:15-36, 146-181); run_Viterbi_spec(seq) runs the chunked recurrence
-// (:50-97).  Results are bit-identical to GraphBLAS_spec_impl(level).
+// implementation GraphBLAS_spec_impl.cpp).  spec_with(hmm) uploads the model and prepares level
+// `level` (GraphBLAS_spec_impl.cpp:15-36, 146-181): level 2 evaluates each chunk's product on chip
+// from the folded sparse matrices, nothing precomputed (the pipelined latency plan for MSV-shaped
+// models with every score >= 0, spec2_kernel otherwise and for the rows the pipelined pass flags;
+// DESIGN.md 5h, 5j); level >= 3 precomputes the emit_num^level dense products in HBM.
+// run_Viterbi_spec(seq) runs the chunked recurrence (:50-97).  Results are bit-identical to
+// GraphBLAS_spec_impl(level).
 //
 // Error behaviour: the reference throws std::out_of_range from unordered_map::at for an
 // unknown symbol chunk (:74); here any out-of-range symbol throws std::out_of_range.

@@ -77,14 +77,19 @@ enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2, SVH_KE
 /* PIPE: the pipelined chain kernel (MSV-shaped models whose feeder row N takes terms only from
  * the light rows and itself): a sequence's states are split over many waves and CUs; N's light
  * term is speculated away and checked exactly at every observation, and a sequence that fails
- * the check is re-run by the serial chain kernel (same results either way).  AUTO uses it for
+ * the check is re-run exactly (scores: inside the same launch by the row's combining workgroup;
+ * paths and the wide plan: by the serial chain kernel) -- the same results either way.  AUTO uses it for
  * scores-only passes over batches too small to fill the chip with the chain kernel.
  * PIPE_WIDE: the same recurrence with one block of states per workgroup and one sequence per wave
  * (the block's table in LDS, shared by the waves): the throughput plan AUTO uses for wider
  * batches.
  * SPEC2 (reported by svh_batch_plan only, not selectable): _spec level 2 evaluated on chip from
  * the folded sparse matrices, one workgroup per sequence (spec2.hip); the odd last observation of
- * a sequence runs on the step kernels. */
+ * a sequence runs on the step kernels.
+ * SPEC2_PIPE (reported by svh_batch_plan only): _spec level 2 on the pipelined latency plan
+ * (pipe_l2.hip: every chunk of every row in one launch, the light term of N and its two-hop terms
+ * speculated away and checked exactly, flagged rows re-run by spec2.hip); AUTO and PIPE use it for
+ * MSV-shaped models whose scores are all >= 0. */
 
 typedef struct {
     int32_t device;      /* HIP device ordinal; -1 = the caller's current device */
@@ -187,12 +192,21 @@ int svh_host_free(void* p);
 int svh_batch_device_results(svh_batch_t b, float** scores, int64_t** best_state);
 /* Milliseconds between the start and stop events of the last svh_batch_run (synchronises). */
 int svh_batch_elapsed_ms(svh_batch_t b, float* ms);
+/* Measurement (the latency plan's roofline): milliseconds per launch, mean of `reps`,
+ * of the batch's pipelined latency pass with every boundary exchange removed -- each wave sweeps
+ * its block as the first block does, with no input from its neighbours and no waits -- so the
+ * launch takes the step's own per-observation time plus the prologue.  Its scores go to a scratch
+ * buffer (they are not the batch's results, which this call leaves untouched).  SVH_E_UNSUPPORTED
+ * unless the batch's scores-only plan is the pipelined latency plan at its default table mode.
+ * Synchronous. */
+int svh_batch_step_floor_ms(svh_batch_t b, void* stream, uint32_t reps, float* ms);
 /* The plan svh_batch_run(level) launches for this batch (its sequence count and paths flag
  * decide between the narrow and the wide chain plan): kernel/threads/slots of the model info. */
 int svh_batch_plan(svh_batch_t b, uint32_t level, svh_model_info* info);
-/* Rows of the last run whose pipelined pass (SVH_KERNEL_PIPE) failed its speculation check and
- * were re-run by the serial chain kernel (results are identical either way); 0 if the last run
- * did not use the pipelined kernel.  Waits for the run. */
+/* Rows of the last run whose pipelined pass (SVH_KERNEL_PIPE, _PIPE_WIDE, _SPEC2_PIPE) failed its
+ * speculation check and were re-run exactly (in the same launch, by the serial chain kernel, or at
+ * level 2 by the on-chip chunk kernel; results are identical either way); 0 if the last run did
+ * not use a pipelined kernel.  Waits for the run. */
 int svh_batch_fallbacks(svh_batch_t b, uint64_t* rows);
 /* Whether this build holds the pipelined latency kernel at `slots` x `waves` with step table mode
  * `table_mode` (pipe_kernel.h TM; SVH_PIPE_SM / SVH_PIPE_WAVES / SVH_PIPE_TM select them).  The

@@ -94,6 +94,7 @@ SIGNATURES = {
     "svh_host_free": (c_int, [c_void_p]),
     "svh_batch_device_results": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
     "svh_batch_elapsed_ms": (c_int, [c_void_p, P_f32]),
+    "svh_batch_step_floor_ms": (c_int, [c_void_p, c_void_p, c_uint32, P_f32]),
     "svh_batch_plan": (c_int, [c_void_p, c_uint32, POINTER(svh_model_info)]),
     "svh_batch_fallbacks": (c_int, [c_void_p, P_u64]),
     "svh_pipe_variant_built": (c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, POINTER(ctypes.c_int32)]),

@@ -255,7 +255,10 @@ bool pipe_supported(int sm, int waves, bool sx);
 // the other geometries only in SVH_PIPE_AB_ALL builds)
 bool pipe_tm_supported(int tm);
 // b.cmask != nullptr selects the decoded-path variant (every sequence must start at step 0).
-hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
+// step_floor: the FLOOR variant (pipe_kernel.h; TM 4 geometry only): the sweep without any exchange,
+// for svh_batch_step_floor_ms (b's outputs must be scratch)
+hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream,
+                       bool step_floor = false);
 // _spec level 2 on the latency plan's geometry (pipe_l2.hip: pipe_kernel.h with L2): every chunk of
 // two observations of every row, from observation 0, into b.scores (dense rows; best states when
 // b.best); rows whose speculation fails are flagged in x.viol (re-run by spec2_kernel, runtime.cpp).

@@ -42,16 +42,20 @@ const void* pipe_kernel_tm0(int sm, int waves, bool sx, int paths) {
 bool pipe_supported(int sm, int waves, bool sx) { return pipe_kernel_tm0(sm, waves, sx, 0) != nullptr; }
 bool pipe_tm_supported(int tm) {
     if (tm == 0) return true;
+    if (tm == -8) return pipe_kernel_tm1(2, 8, false, -4) != nullptr;  // TM 4 at 8 waves (A/B builds)
     return tm >= 1 && tm <= 4 && pipe_kernel_tm1(2, 4, false, tm >= 2 ? -tm : 0) != nullptr;
 }
 bool pipe_paths_supported(int sm, int waves) { return pipe_kernel_tm0(sm, waves, false, 1) != nullptr; }
 
-hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream) {
+hipError_t launch_pipe(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream,
+                       bool step_floor) {
     const bool paths = b.cmask != nullptr;
     const int pv = paths ? (m.ties_heavy ? 2 : 1) : 0;
     // TM = 1 (pair tables) needs 2 slots per lane and at most kPairSym symbols
     if (m.tm && (m.SM != 2 || m.S > kPairSym)) return hipErrorInvalidValue;
-    const void* fn = !m.tm ? pipe_kernel_tm0((int)m.SM, (int)m.W, m.sx != 0, pv)
+    if (step_floor && (paths || m.tm != 4 || m.W != 4)) return hipErrorInvalidValue;
+    const void* fn = step_floor ? pipe_kernel_floor(m.sx != 0)
+                     : !m.tm ? pipe_kernel_tm0((int)m.SM, (int)m.W, m.sx != 0, pv)
                      : paths ? pipe_kernel_tm1_paths((int)m.SM, (int)m.W, m.sx != 0, pv, m.tm == 4 ? 4 : 1)
                              : pipe_kernel_tm1((int)m.SM, (int)m.W, m.sx != 0, m.tm >= 2 ? -(int)m.tm : 0);
     if (!fn || m.S > 32 || m.G == 0 || m.nblk > m.G * m.W || m.P != m.nblk * 64 * m.SM || !x.ctr ||

@@ -446,7 +446,10 @@ __device__ __forceinline__ void pipe_rerun_row(const PipeModel& m, const FusedBa
     }
 }
 
-template <int SM, int W, bool SX, int PATHS, int TM, bool L2 = false>
+// FLOOR (svh_batch_step_floor_ms): every wave sweeps its block as block 0 does -- no boundary input,
+// no exchange, no waits -- so the launch times the step alone (the per-observation issue floor of
+// one wave); its scores are meaningless and go to a scratch buffer.
+template <int SM, int W, bool SX, int PATHS, int TM, bool L2 = false, bool FLOOR = false>
 __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     static_assert(TM == 0 || SM == 2, "pair tables: two slots per lane");
     static_assert(TM >= 0 && TM <= 4, "table mode");
@@ -1500,7 +1503,9 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             }
         };
 
-        if (len > first && dbg && (m.diag & 1u)) {
+        if (FLOOR) {
+            if (len > first) sweep(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+        } else if (len > first && dbg && (m.diag & 1u)) {
             sweep(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});  // no exchange (timing only)
         } else if (len > first) {
             using I0 = std::integral_constant<int, 0>;
@@ -1595,7 +1600,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
             if (b.best) b.best[q] = bk2 == kNoRow ? -1 : (int64_t)bk2;
             x.viol[q] = vi;
             __hip_atomic_store(x.done + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            rr = !PATHS && !L2 && m.rerun && vi;  // this workgroup re-runs the row (below)
+            rr = !PATHS && !L2 && !FLOOR && m.rerun && vi;  // this workgroup re-runs the row (below)
         }
         *tick = rr ? 1u : 0u;  // (the ticket itself is in id since the first barrier)
     }
@@ -1620,5 +1625,6 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
 const void* pipe_kernel_tm0(int sm, int waves, bool sx, int paths);
 const void* pipe_kernel_tm1(int sm, int waves, bool sx, int paths);
 const void* pipe_kernel_tm1_paths(int sm, int waves, bool sx, int paths, int tm);
+const void* pipe_kernel_floor(bool sx);
 
 }  // namespace svh

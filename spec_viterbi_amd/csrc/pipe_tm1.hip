@@ -12,6 +12,12 @@
 
 namespace svh {
 
+// The step-floor variant of the default (TM = 4) scores kernel (pipe_kernel.h FLOOR).
+const void* pipe_kernel_floor(bool sx) {
+    return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 4, false, true>)
+              : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 4, false, true>);
+}
+
 const void* pipe_kernel_tm1(int sm, int waves, bool sx, int paths) {
     if (sm != 2 || (paths && (paths < -4 || paths > -2))) return nullptr;
 #ifdef SVH_PIPE_AB_ONLY  // A/B timing builds: the headline geometry only
@@ -20,11 +26,17 @@ const void* pipe_kernel_tm1(int sm, int waves, bool sx, int paths) {
     if (paths == -4) return waves == 4 && !sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 4>) : nullptr;
     return waves == 4 && !sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 1>) : nullptr;
 #else
+#ifndef SVH_PIPE_AB_ALL
     if (waves != 4) return nullptr;
-    if (paths == -4)  // TM = 4 (indexed operands, packed feeder terms): the mode AUTO selects
+#endif
+    if (paths == -4 && waves == 4)  // TM = 4 (indexed operands, packed feeder terms): the mode AUTO selects
         return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 4>)
                   : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 4>);
 #ifdef SVH_PIPE_AB_ALL  // A/B and table-mode-test builds: the modes measured against it
+    if (paths == -4 && waves == 8)  // TM = 4 at 8 waves per workgroup (two per SIMD: 3 workgroups per row)
+        return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 8, true, 0, 4>)
+                  : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 8, false, 0, 4>);
+    if (waves != 4) return nullptr;
     if (paths == -2)  // TM = 2 (indexed operands; SVH_PIPE_TM=2)
         return sx ? reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, true, 0, 2>)
                   : reinterpret_cast<const void*>(&pipe_viterbi_kernel<2, 4, false, 0, 2>);

@@ -798,7 +798,7 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     // 0.255 ms on the headline against 0.263 / 0.268 / 0.277 for TM 2 / 3 / 1 and 0.334 for the
     // per-slot tables); SVH_PIPE_TM selects another mode (A/B and tests: 0 per-slot
     // tables, 1 pair tables by 64-bit moves, 2 indexed operands, 3 packed feeder terms, 4 both)
-    view.tm = !p.wide && p.SM == 2 && p.W == 4 && S <= kPairSymbols ? 4u : 0u;
+    view.tm = !p.wide && p.SM == 2 && (p.W == 4 || (p.W == 8 && pipe_tm_supported(-8))) && S <= kPairSymbols ? 4u : 0u;
     if (const char* e = std::getenv("SVH_PIPE_TM"); e) {
         const int t = std::atoi(e);
         if (t == 0 || (t >= 1 && t <= 4 && view.tm && pipe_tm_supported(t))) view.tm = (uint32_t)t;
@@ -2301,6 +2301,50 @@ uint64_t Batch::pipe_fallbacks() {
     uint64_t c = 0;
     for (uint32_t q = 0; q < nseq; ++q) c += (v[q] | v2[q]) != 0;
     return c;
+}
+
+float Batch::step_floor_ms(hipStream_t s, uint32_t reps) {
+    std::lock_guard<std::mutex> lock(model->mu);
+    DeviceGuard g(model->device);
+    if (!s) s = model->stream;
+    const DevicePipePlan* pp = model->pipe_for(nseq);
+    if (!pp || pp->plan.wide || pp->view.tm != 4 || pp->plan.W != 4 || !model->band_for(false, nseq))
+        throw Error(SVH_E_UNSUPPORTED, "step floor: the batch's plan is not the pipelined latency plan (TM 4)");
+    floor_scratch.ensure(nseq, pp->plan.G, s);
+    const size_t n = model->host.n;
+    d_floor_out.reserve(16 + (size_t)nseq * n * 4);
+    FusedBatch fb;
+    std::memset(&fb, 0, sizeof(fb));
+    fb.symbols = p_sym;
+    fb.sym_off = p_symoff;
+    fb.begin = p_begin;
+    fb.end = p_end;
+    fb.fault = d_floor_out.as<uint32_t>();
+    fb.scores = reinterpret_cast<float*>(d_floor_out.as<uint8_t>() + 16);
+    fb.nseq = nseq;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hip_check(hipEventCreate(&e0), "hipEventCreate");
+    hip_check(hipEventCreate(&e1), "hipEventCreate");
+    float ms = 0;
+    try {
+        floor_scratch.note_launch(s);
+        hip_check(launch_pipe(pp->view, fb, floor_scratch.view, s, true), "step-floor kernel (warm-up)");
+        hip_check(hipEventRecord(e0, s), "hipEventRecord");
+        for (uint32_t r = 0; r < reps; ++r) {
+            floor_scratch.note_launch(s);
+            hip_check(launch_pipe(pp->view, fb, floor_scratch.view, s, true), "step-floor kernel");
+        }
+        hip_check(hipEventRecord(e1, s), "hipEventRecord");
+        hip_check(hipEventSynchronize(e1), "hipEventSynchronize");
+        hip_check(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+    } catch (...) {
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        throw;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return ms / (float)reps;
 }
 
 float Batch::elapsed_ms() {

@@ -326,6 +326,11 @@ struct Batch {
     void run(uint32_t level, hipStream_t s);
     void read(hipStream_t s, float* scores, int64_t* best, int32_t* paths);
     float elapsed_ms();
+    // the latency plan's pass with no boundary exchange (FLOOR), ms per launch over `reps` (its own
+    // scratch and outputs; svh_batch_step_floor_ms)
+    float step_floor_ms(hipStream_t s, uint32_t reps);
+    PipeScratchBuffers floor_scratch;
+    DeviceBuffer d_floor_out;
     // rows of the last run that the pipelined kernel handed to the serial kernel (synchronous)
     uint64_t pipe_fallbacks();
     bool pipe_ran = false;  // the last run used the pipelined kernel

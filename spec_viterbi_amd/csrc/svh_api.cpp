@@ -279,6 +279,13 @@ int svh_batch_elapsed_ms(svh_batch_t b, float* ms) {
     });
 }
 
+int svh_batch_step_floor_ms(svh_batch_t b, void* stream, uint32_t reps, float* ms) {
+    return guarded([&] {
+        require(b && ms && reps > 0, "null argument or reps == 0");
+        *ms = b->impl->step_floor_ms(static_cast<hipStream_t>(stream), reps);
+    });
+}
+
 int svh_batch_fallbacks(svh_batch_t b, uint64_t* rows) {
     return guarded([&] {
         require(b && rows, "null argument");

@@ -222,6 +222,14 @@ class DeviceBatch:
         up; this batch's next read() raises, other batches of the model are unaffected."""
         _lib.check(_lib.lib.svh_batch_debug_fault(self._h, ctypes.c_void_p(stream or 0)))
 
+    def step_floor_ms(self, reps: int = 10, stream: int | None = None) -> float:
+        """The latency plan's pass with every boundary exchange removed (svh_batch_step_floor_ms):
+        the step's own per-observation time, the roofline the exchange is measured against.  Leaves
+        the batch's results untouched."""
+        ms = ctypes.c_float()
+        _lib.check(_lib.lib.svh_batch_step_floor_ms(self._h, ctypes.c_void_p(stream or 0), int(reps), ctypes.byref(ms)))
+        return float(ms.value)
+
     def elapsed_ms(self) -> float:
         ms = ctypes.c_float()
         _lib.check(_lib.lib.svh_batch_elapsed_ms(self._h, ctypes.byref(ms)))

@@ -579,3 +579,31 @@ def test_pipew_paths_replicated_headline_digests(copies):
         assert hashlib.sha256(np.asarray(pth[q], np.int32).tobytes()).hexdigest() == r["path_sha256"], q
     batch.close()
     model.close()
+
+
+def test_step_floor_measurement_and_untimed_batches():
+    """svh_batch_step_floor_ms (the latency plan without its boundary exchange, bench.py's
+    roofline.latency) returns a positive time below the real pass and leaves the batch's results,
+    fault word and fallback flags untouched; a batch created with SVH_BATCH_NO_TIMING (timing=False)
+    runs without its own events, reports fallbacks by waiting on the run's stream and refuses
+    elapsed_ms()."""
+    hmm = svh.read_HMM(chmm("2405.chmm"))
+    seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
+    model = svh.DeviceModel(hmm)
+    batch = model.batch(seqs, timing=False)
+    batch.run()
+    s1, b1 = batch.read()
+    floor = batch.step_floor_ms(5)
+    assert floor > 0
+    s2, b2 = batch.read()
+    assert np.array_equal(s1.view(np.uint32), s2.view(np.uint32)) and np.array_equal(b1, b2)
+    assert batch.fallbacks() == 0
+    with pytest.raises(_lib.SvhError) as e:
+        batch.elapsed_ms()
+    assert e.value.code == _lib.SVH_E_STATE
+    timed = model.batch(seqs)
+    timed.run()
+    assert floor < timed.elapsed_ms()
+    g = load_golden("chmm2405_emit50")
+    for rec in g["sequences"]:
+        assert bit_equal(s1[rec["index"]], from_hex(rec["scores"]))
