@@ -48,14 +48,20 @@ $(LIB): $(OBJS) $(BUILD)/pipe.hazards
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
 # The pipelined kernel's inline-asm DPP reads rely on the schedule for one of their two wait
-# states: every build checks all of them in the gfx950 code objects (tools/dpp_hazards.py).
+# states: every build checks all of them in the gfx950 code objects (tools/dpp_hazards.py).  Its
+# asm granule prefetches must not be read (copied, spilled) before their wait: every build checks
+# them in the compiler's assembly output, where inline asm is marked (tools/check_prefetch.py).
 PIPE_OBJS := pipe pipe_tm1 pipe_tm1p pipe_l2
-$(BUILD)/pipe.hazards: $(foreach o,$(PIPE_OBJS),$(BUILD)/$(o).o) tools/dpp_hazards.py
+$(BUILD)/%.dev.s: $(CSRC)/%.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o $@
+$(BUILD)/pipe.hazards: $(foreach o,$(PIPE_OBJS),$(BUILD)/$(o).o $(BUILD)/$(o).dev.s) tools/dpp_hazards.py tools/check_prefetch.py
 	set -e; for o in $(PIPE_OBJS); do \
 	  (cd $(BUILD) && /opt/rocm/lib/llvm/bin/llvm-objdump --offloading $$o.o > /dev/null); \
 	  co=$(BUILD)/$$o.o.0.hipv4-amdgcn-amd-amdhsa--gfx950; [ -f $$co ] || continue; \
 	  /opt/rocm/lib/llvm/bin/llvm-objdump -d $$co > $(BUILD)/$$o.s; \
-	  python3 tools/dpp_hazards.py $(BUILD)/$$o.s pipe_viterbi_kernel; done > $@
+	  python3 tools/dpp_hazards.py $(BUILD)/$$o.s pipe_viterbi_kernel; \
+	  python3 tools/check_prefetch.py $(BUILD)/$$o.dev.s; done > $@.tmp
+	mv $@.tmp $@
 
 # Oracle: plain C, every add rounded on its own (test infrastructure only).
 $(ORACLE): oracle/viterbi_oracle.c oracle/viterbi_oracle.h

@@ -594,12 +594,17 @@ def main(argv=None):
         else:
             ess_b = algo if args.level >= 2 else essential_bytes_per_launch(n, int(info["S"]), lengths, args.paths)
         rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc, ess_b)
+        floor_ms = None
         if plan["kernel"] == 5 and not args.paths and args.level <= 1 and batch:
             # the latency plan's own floor, measured live: the same launch with every boundary exchange
             # removed (svh_batch_step_floor_ms: each wave sweeps its block with no neighbour input and no
             # waits), i.e. the step's per-observation issue time at one wave per SIMD plus the prologue
-            floor_ms = batch.step_floor_ms(10, sptr)
+            try:
+                floor_ms = batch.step_floor_ms(10, sptr)
+            except svh._lib.SvhError:  # an A/B geometry without the floor variant (SVH_PIPE_WAVES)
+                floor_ms = None
             maxlen = max(lengths)
+        if floor_ms is not None:
             rl["latency_frac"] = round(floor_ms / kernel_ms, 4)
             rl["latency"] = {"step_floor_ms": round(floor_ms, 4), "frac": rl["latency_frac"],
                              "floor_ns_per_observation": round(floor_ms * 1e6 / maxlen, 2),

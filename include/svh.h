@@ -208,6 +208,9 @@ int svh_batch_plan(svh_batch_t b, uint32_t level, svh_model_info* info);
  * level 2 by the on-chip chunk kernel; results are identical either way); 0 if the last run did
  * not use a pipelined kernel.  Waits for the run. */
 int svh_batch_fallbacks(svh_batch_t b, uint64_t* rows);
+/* The same per row: flags[q] (nseq words) bit 0 = the step pass re-ran row q, bit 1 = the _spec
+ * level-2 pass on the pipelined plan handed it to the on-chip chunk kernel.  Waits for the run. */
+int svh_batch_fallback_rows(svh_batch_t b, uint32_t* flags);
 /* Whether this build holds the pipelined latency kernel at `slots` x `waves` with step table mode
  * `table_mode` (pipe_kernel.h TM; SVH_PIPE_SM / SVH_PIPE_WAVES / SVH_PIPE_TM select them).  The
  * default build holds the geometry and modes AUTO plans (2 x 4; TM 4, and TM 0 for alphabets of

@@ -68,6 +68,7 @@ P_u64 = POINTER(c_uint64)
 P_f32 = POINTER(c_float)
 P_i64 = POINTER(c_int64)
 P_i32 = POINTER(c_int32)
+P_u32 = POINTER(c_uint32)
 
 # name -> (restype, argtypes); every function declared in include/svh.h.
 SIGNATURES = {
@@ -95,6 +96,7 @@ SIGNATURES = {
     "svh_batch_device_results": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
     "svh_batch_elapsed_ms": (c_int, [c_void_p, P_f32]),
     "svh_batch_step_floor_ms": (c_int, [c_void_p, c_void_p, c_uint32, P_f32]),
+    "svh_batch_fallback_rows": (c_int, [c_void_p, P_u32]),
     "svh_batch_plan": (c_int, [c_void_p, c_uint32, POINTER(svh_model_info)]),
     "svh_batch_fallbacks": (c_int, [c_void_p, P_u64]),
     "svh_pipe_variant_built": (c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, POINTER(ctypes.c_int32)]),

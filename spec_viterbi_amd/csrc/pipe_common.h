@@ -43,5 +43,18 @@ __device__ __forceinline__ void g_prefetch64(uint64_t& dst, const uint64_t* p) {
     asm volatile("global_load_dwordx2 %0, %1, off sc1" : "+v"(dst) : "v"(p) : "memory");
 }
 
+// The last workgroup of a launch to finish (every one has taken its ticket and read the epoch):
+// tickets and the finish count back to 0, the epoch advanced (ctr[2] + 1 is this launch's).
+__device__ __forceinline__ void pipe_reset_counters(const PipeScratch& x) {
+    const uint32_t ep = __hip_atomic_load(x.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __hip_atomic_store(x.ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(x.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t c = kCtrClass; c <= kCtrLeft; ++c) __hip_atomic_store(x.ctr + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(x.ctr + 2, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// hwreg(HW_REG_XCC_ID, 0, 4): the XCD this wave runs on (the XCD-local hand-offs, SVH_PIPE_XL)
+__device__ __forceinline__ uint32_t xcc_id() { return (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xFu; }
+
 }  // namespace pipe_dev
 }  // namespace svh

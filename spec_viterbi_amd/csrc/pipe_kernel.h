@@ -182,6 +182,40 @@ constexpr bool kNoPRing = true;
 constexpr bool kNoPRing = false;
 #endif
 
+// Slow-path loads that wait for themselves (SVH_PIPE_SYNCSLOW, default 1): the compiler tracks every
+// load it emits, so a poll loop's reload left pending where the slow path rejoins the body made it
+// drain every outstanding operation there -- on the fast path too: the granule consumer's body then
+// waited with vmcnt(0) for the next group's prefetch once per group, and the LDS consumers'
+// re-read of a boundary vector forced an lgkmcnt wait behind the ring stores.  A load whose wait is
+// inside its own asm leaves nothing for the compiler to drain (the wide kernel's g_ld64_sync).
+#ifndef SVH_PIPE_SYNCSLOW
+#define SVH_PIPE_SYNCSLOW 1
+#endif
+__device__ __forceinline__ uint64_t g_ld64_slow(const uint64_t* p) {
+    if constexpr (SVH_PIPE_SYNCSLOW) {
+        uint64_t r;
+        asm volatile("global_load_dwordx2 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+        return r;
+    }
+    return g_ld64(p);
+}
+__device__ __forceinline__ uint32_t lds_ld32_slow(const uint32_t* p) {
+    if constexpr (SVH_PIPE_SYNCSLOW) {
+        uint32_t r;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(lds_addr(p)) : "memory");
+        return r;
+    }
+    return lds_ld32(p);
+}
+__device__ __forceinline__ float lds_ldf_slow(const float* p) {
+    if constexpr (SVH_PIPE_SYNCSLOW) {
+        float r;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(lds_addr(p)) : "memory");
+        return r;
+    }
+    return *p;
+}
+
 // One lane's LDS store of a wave-uniform word (a wave's count): EXEC narrowed to lane 0 inside the
 // asm (no divergent branch in the compiler's view).  Measured and not kept (round 4): every lane
 // storing, lanes 1..63 into a sink of their own (no EXEC writes), within noise.
@@ -325,15 +359,6 @@ __device__ __forceinline__ float shr_in(float v, float bvv) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(old, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
 }
 
-// The last workgroup of a launch to finish (every one has taken its ticket and read the epoch):
-// tickets and the finish count back to 0, the epoch advanced (ctr[2] + 1 is this launch's).
-__device__ __forceinline__ void pipe_reset_counters(const PipeScratch& x) {
-    const uint32_t ep = __hip_atomic_load(x.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    __hip_atomic_store(x.ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(x.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t c = kCtrClass; c <= kCtrLeft; ++c) __hip_atomic_store(x.ctr + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(x.ctr + 2, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Exact serial re-run of row q whose speculation failed (m.rerun: the scores variant of the latency
 // plan, P small enough for the ring's LDS), by the workgroup that combines the row, so that no
@@ -1155,7 +1180,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         // wait until the previous wave has published observations < need
         auto wait_prev = [&](uint32_t need) {
             if (kNoWait) return;
-            while ((uint32_t)uniform((int)lds_ld32(cnt_w - 1)) < need) {
+            while ((uint32_t)uniform((int)lds_ld32_slow(cnt_w - 1)) < need) {
                 if (dbg) ++dg[3];
                 if (give_up()) break;
                 __builtin_amdgcn_s_sleep(1);
@@ -1164,7 +1189,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         // flow control: the next wave has consumed observations < need
         auto wait_next = [&](uint32_t need) {
             if (kNoWait) return;
-            while ((int)uniform((int)lds_ld32(cnt_w + 1)) < (int)need) {
+            while ((int)uniform((int)lds_ld32_slow(cnt_w + 1)) < (int)need) {
                 if (dbg) ++dg[4];
                 if (give_up()) break;
                 __builtin_amdgcn_s_sleep(1);
@@ -1201,12 +1226,12 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         };
         auto wait_cons = [&](uint32_t need) {
             if (kNoWait) return;
-            uint64_t c = g_ld64(cons_out);
+            uint64_t c = g_ld64_slow(cons_out);
             while (!cons_ok(uni64(c), need)) {
                 if (dbg) ++dg[6];
                 if (give_up()) break;
                 __builtin_amdgcn_s_sleep(2);
-                c = g_ld64(cons_out);
+                c = g_ld64_slow(cons_out);
             }
         };
         auto put_gran1 = [&](uint32_t s, float val) {  // single observation (slow path), lane 0 stores
@@ -1218,6 +1243,17 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         // The sweep, with the boundary roles as compile-time constants (one code path per role).
         auto sweep = [&](auto srcc, auto dstc) {
             constexpr uint32_t GPF = kGpf;  // granule groups in flight (SRC 2)
+            // The granule prefetch is an asm load into a loop-carried register (g_prefetch64) where
+            // the register budget leaves the compiler no reason to move it; the level-2 body runs at
+            // the 256-VGPR limit and copied the pending register to an AGPR before the load landed
+            // (a stale granule then passed the lap tag, and the late return can overwrite a
+            // re-used register), so there the prefetch is a load the compiler tracks.
+            // tools/check_prefetch.py rejects a build whose asm prefetch is read before its wait.
+            constexpr bool kPfAsm = !L2;
+            auto prefetch = [&](uint64_t& d, const uint64_t* p) {
+                if constexpr (kPfAsm) g_prefetch64(d, p);
+                else d = g_ld64(p);
+            };
             constexpr int SRC = decltype(srcc)::value, DST = decltype(dstc)::value;
             // one observation outside the unrolled groups: per-observation waits
             auto single = [&](uint32_t t) {
@@ -1299,7 +1335,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                 uint64_t gq[GPF] = {};  // SRC 2: granule groups in flight
                 if constexpr (SRC == 2) {
 #pragma unroll
-                    for (uint32_t j = 0; j < GPF; ++j) g_prefetch64(gq[j], gin + ((t + 8 * j + (lane & 7u)) & (kGR - 1)));
+                    for (uint32_t j = 0; j < GPF; ++j) prefetch(gq[j], gin + ((t + 8 * j + (lane & 7u)) & (kGR - 1)));
                 }
                 float gpend = 0.0f;    // DST 2: the previous group's boundary scores (lanes 0..7),
                 uint32_t gpend_t = 0;  // read back from the ring one group before they are stored
@@ -1356,16 +1392,16 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                         float bv = kInf;  // lanes 0..7: the previous block's last scores of tg..tg+7
                         float gl[8];      // SVH_PIPE_RING8: this group's last-slot scores
                         if constexpr (SRC == 2) {
-                            wait_vmcnt<GPF - 1>();  // gq[j]: GPF - 1 later loads in flight
+                            if constexpr (kPfAsm) wait_vmcnt<GPF - 1>();  // gq[j]: GPF - 1 later loads in flight
                             uint64_t gv = gq[j % GPF];
                             while (!kNoWait && __builtin_amdgcn_ballot_w64((uint32_t)(gv >> 32) != gtag(ep, tg)) != 0) {
                                 if (dbg) ++dg[5];
                                 if (give_up()) break;
                                 __builtin_amdgcn_s_sleep(1);
-                                gv = g_ld64(gin + ((tg + (lane & 7u)) & (kGR - 1)));
+                                gv = g_ld64_slow(gin + ((tg + (lane & 7u)) & (kGR - 1)));
                             }
                             bv = __builtin_bit_cast(float, (uint32_t)gv);
-                            g_prefetch64(gq[j % GPF], gin + ((tg + 8 * GPF + (lane & 7u)) & (kGR - 1)));
+                            prefetch(gq[j % GPF], gin + ((tg + 8 * GPF + (lane & 7u)) & (kGR - 1)));
                         }
                         if constexpr (DST == 1) {
                             if constexpr (SVH_PIPE_LDSX) asm volatile("" : "+v"(nc_rd));
@@ -1381,7 +1417,7 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
                                     if constexpr (SVH_PIPE_LDSX) asm volatile("v_mov_b32 %0, 0" : "=v"(z));
                                     wait_prev(tg + 8);
                                     asm volatile("" ::: "memory");
-                                    bv_next = ring_prev[ring_idx(8 * j + (lane & 7u), 63) + z];
+                                    bv_next = lds_ldf_slow(ring_prev + ring_idx(8 * j + (lane & 7u), 63) + z);
                                 }
                             }
                             if constexpr (SRC == 1) bv = bv_next;

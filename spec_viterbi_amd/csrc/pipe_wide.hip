@@ -3,6 +3,8 @@
 // instantiates the decoded-path variants.
 #include "pipe_wide_kernel.h"
 
+#include <cstdlib>
+
 namespace svh {
 
 namespace {
@@ -61,7 +63,13 @@ hipError_t launch_pipew(const PipeModel& m, const FusedBatch& b, const PipeScrat
     PipeScratch xx = x;
     const void* hc = m.hc;
     void* args[] = {&mm, &bb, &xx, &hc};
-    const uint64_t grid = ((uint64_t)b.nseq + W - 1) / W * m.nblk;
+    uint64_t groups = ((uint64_t)b.nseq + W - 1) / W;
+    // XCD classes (pipe_wide_kernel.h): groups padded to a multiple of 8, class r = b % 8 takes a
+    // contiguous eighth of them; SVH_PIPEW_XMAP=0 keeps the single ticket counter (A/B)
+    static const bool xmap_env = !(std::getenv("SVH_PIPEW_XMAP") && std::atoi(std::getenv("SVH_PIPEW_XMAP")) == 0);
+    xx.xmap = xmap_env ? 1u : 0u;
+    if (xx.xmap) groups = (groups + 7) & ~7ull;
+    const uint64_t grid = groups * m.nblk;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
     return hipLaunchKernel(fn, dim3((uint32_t)grid), dim3(64 * W), args, lds, stream);
 }

@@ -20,6 +20,14 @@
 // four groups of 8 ahead, tag-checked; flow control through the consumer's progress word).
 // Workgroups take dynamic tickets (sequence group major, block minor), so a consumer's producer
 // has always started: no deadlock beyond residency while nblk workgroups fit on the chip.
+// XCD classes (x.xmap, round 6; the latency plan's §5f scheme for a grid of any size): the grid is
+// padded to a multiple of 8 nblk and workgroup b takes its ticket from the counter of class
+// r = b % 8 (blocks b and b + 8 share an XCD under the observed round-robin placement), whose
+// tickets map to a contiguous range of sequence groups, so a group's nblk workgroups share an L2.
+// Each workgroup publishes its XCC id; a granule producer whose consumer is on its own XCD stores
+// with plain (L2-resident) stores, and so does a consumer with its progress word (SVH_PIPEW_XL);
+// otherwise, or when the other's id is not known in time, agent-scope write-through stores.  Per
+// class the tickets are still taken in start order, so a consumer's producer has always started.
 // Each wave combines its own lanes (S partial, argmin, violation); the last wave of a sequence
 // to finish combines the blocks.
 //
@@ -33,6 +41,13 @@
 // shuffles) and lanes 0..7 store prec[block][t].  pipe_paths.hip walks the paths from them.
 #pragma once
 #include "pipe_common.h"
+
+// XCD classes and XCD-local hand-offs for the wide plan (A/B knobs; header comment): the launch's
+// row mapping (PipeScratch::xmap, launch_pipew; SVH_PIPEW_XMAP=0 at run time turns it off) and the
+// plain stores between workgroups on one XCD.
+#ifndef SVH_PIPEW_XL
+#define SVH_PIPEW_XL 1
+#endif
 
 namespace svh {
 
@@ -93,7 +108,17 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t w = (uint32_t)uniform((int)(tid >> 6));
-    if (tid == 0) *tick = __hip_atomic_fetch_add(x.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+        uint32_t t;
+        if (x.xmap) {  // class r = b % 8: groups [r gpc, (r + 1) gpc), tickets in start order
+            const uint32_t r = blockIdx.x & 7u, gpc = (gridDim.x >> 3) / nblk;
+            const uint32_t k = __hip_atomic_fetch_add(x.ctr + kCtrClass + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            t = (r * gpc + k / nblk) * nblk + k % nblk;
+        } else {
+            t = __hip_atomic_fetch_add(x.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *tick = t;
+    }
     __syncthreads();
     const uint32_t id = (uint32_t)uniform((int)*tick);
     const uint32_t qg = id / nblk, blk = id - qg * nblk;
@@ -106,6 +131,11 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
     __syncthreads();
     const uint32_t ep = (uint32_t)uniform((int)__hip_atomic_load(x.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
     const uint32_t q = qg * W + w;
+#if SVH_PIPEW_XL
+    const uint32_t my_xcc = xcc_id();
+    if (tid == 0 && x.xcc && qg * W < b.nseq)
+        __hip_atomic_store(x.xcc + (size_t)qg * nblk + blk, (ep << 4) | my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 
     if (q < b.nseq) {
         const uint8_t* __restrict__ sym = b.symbols + b.sym_off[q];
@@ -343,14 +373,42 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
                 c = g_ld64_sync(cons_out);
             }
         };
+        // SVH_PIPEW_XL: is block ob of this group on this wave's XCD?  (a bounded poll of its id; not
+        // known in time: no, i.e. write-through stores, always correct)
+        auto xcc_local = [&](uint32_t ob) -> bool {
+#if SVH_PIPEW_XL
+            if (!x.xcc) return false;
+            const uint32_t* p = x.xcc + (size_t)qg * nblk + ob;
+            for (int i = 0; i < 32; ++i) {
+                const uint32_t wv = (uint32_t)uniform((int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if ((wv >> 4) == (ep & 0x0FFFFFFFu)) return (wv & 0xFu) == my_xcc;
+                __builtin_amdgcn_s_sleep(4);
+            }
+#endif
+            (void)ob;
+            return false;
+        };
+        bool gran_plain = false, cons_plain = false;
+        // granule / progress-word stores: plain (a relaxed wavefront-scope atomic store: the same
+        // unflagged global_store, kept in this XCD's L2) when the reader shares this XCD
+        auto st_gran = [&](uint64_t* a, uint64_t v64) {
+            if (SVH_PIPEW_XL && gran_plain) __hip_atomic_store(a, v64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            else g_st64(a, v64);
+        };
+        auto st_cons = [&](uint64_t v64) {
+            if (SVH_PIPEW_XL && cons_plain) __hip_atomic_store(cons_in, v64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            else g_st64(cons_in, v64);
+        };
         auto put_gran1 = [&](uint32_t s, float val) {
             const uint64_t gv = ((uint64_t)gtag(ep, s) << 32) | __builtin_bit_cast(uint32_t, val);
-            if (lane == 0) g_st64(gout + (s & (kGR - 1)), gv);
+            if (lane == 0) st_gran(gout + (s & (kGR - 1)), gv);
         };
 
         auto sweep = [&](auto srcc, auto dstc) {
             constexpr int SRC = decltype(srcc)::value, DST = decltype(dstc)::value;
             using I0 = std::integral_constant<int, 0>;
+            if constexpr (SVH_PIPEW_XL && DST == 2) gran_plain = xcc_local(blk + 1);
+            if constexpr (SVH_PIPEW_XL && SRC == 2) cons_plain = xcc_local(blk - 1);
             // one observation outside the body (head, tail): per-observation exchange
             auto single = [&](uint32_t t) {
                 window_for(t);
@@ -368,7 +426,7 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
                 }
                 if constexpr (SRC == 2) {
                     if (t + 1 < len) bprev = gran_value(t);
-                    if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | (t + 1));
+                    if (lane == 0) st_cons(((uint64_t)ep << 32) | (t + 1));
                 }
             };
             // the granules of a group after a tag miss (slow path: poll until the producer has them)
@@ -391,7 +449,7 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
                 // initial progress (observations < first are done): a row that starts mid-sequence
                 // at a multiple of 64 would otherwise leave its producer's first flow-control wait
                 // on a stale word while this wave waits for that producer's granules
-                if (lane == 0) g_st64(cons_in, ((uint64_t)ep << 32) | first);
+                if (lane == 0) st_cons(((uint64_t)ep << 32) | first);
             }
 
             uint32_t t = first;
@@ -417,7 +475,7 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
                 if constexpr (DST == 2) gpend = ring_w[(lane & 7u) * 64 + 63];
                 uint32_t gpend_t = t - 8;
                 auto store_pending = [&]() {
-                    g_st64(gout + ((gpend_t + (lane & 7u)) & (kGR - 1)),
+                    st_gran(gout + ((gpend_t + (lane & 7u)) & (kGR - 1)),
                            ((uint64_t)gtag(ep, gpend_t) << 32) | __builtin_bit_cast(uint32_t, gpend));
                 };
                 float bv_prev = bprev;  // lane 7 (all lanes) = boundary of t-1
@@ -497,7 +555,7 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
                         }
                         if constexpr (SRC == 2 && j == 3) {
                             asm volatile("" ::: "memory");
-                            g_st64(cons_in, ((uint64_t)ep << 32) | (tg + 8));
+                            st_cons(((uint64_t)ep << 32) | (tg + 8));
                         }
                     };
                     group(std::integral_constant<uint32_t, 0>{}, sw0, sw1);
@@ -592,11 +650,7 @@ __global__ __launch_bounds__(64 * W) void pipew_viterbi_kernel(PipeModel m, Fuse
     __syncthreads();
     if (tid == 0) {  // launch end: the last workgroup resets the tickets and advances the epoch
         const uint32_t f = __hip_atomic_fetch_add(x.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (f == gridDim.x - 1) {
-            __hip_atomic_store(x.ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(x.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(x.ctr + 2, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (f == gridDim.x - 1) pipe_reset_counters(x);  // every workgroup has taken its ticket
     }
 }
 

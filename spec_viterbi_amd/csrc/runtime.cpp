@@ -2288,9 +2288,10 @@ void Batch::inject_fault(hipStream_t s) {
     hip_check(hipMemsetAsync(p_fault, 0x01, 1, s), "fault inject");  // kFaultPipe
 }
 
-uint64_t Batch::pipe_fallbacks() {
+uint64_t Batch::pipe_fallbacks(uint32_t* rows) {
     DeviceGuard g(model->device);
     if (!ran) throw Error(SVH_E_STATE, "no run recorded");
+    if (rows) std::memset(rows, 0, (size_t)nseq * 4);
     if (!pipe_ran && !l2_ran) return 0;
     if (timing) hip_check(hipEventSynchronize(ev_stop), "hipEventSynchronize");
     else hip_check(hipStreamSynchronize(last_stream), "hipStreamSynchronize");
@@ -2299,7 +2300,10 @@ uint64_t Batch::pipe_fallbacks() {
     // level 2 on the pipelined plan: its rows re-run by spec2_kernel count too
     if (l2_ran) hip_check(hipMemcpy(v2.data(), d_l2viol.ptr, (size_t)nseq * 4, hipMemcpyDeviceToHost), "fallback flags D2H");
     uint64_t c = 0;
-    for (uint32_t q = 0; q < nseq; ++q) c += (v[q] | v2[q]) != 0;
+    for (uint32_t q = 0; q < nseq; ++q) {
+        c += (v[q] | v2[q]) != 0;
+        if (rows) rows[q] = (v[q] ? 1u : 0u) | (v2[q] ? 2u : 0u);
+    }
     return c;
 }
 

@@ -332,7 +332,8 @@ struct Batch {
     PipeScratchBuffers floor_scratch;
     DeviceBuffer d_floor_out;
     // rows of the last run that the pipelined kernel handed to the serial kernel (synchronous)
-    uint64_t pipe_fallbacks();
+    // rows (nullable, nseq words): bit 0 the step pass re-ran the row, bit 1 the level-2 pass
+    uint64_t pipe_fallbacks(uint32_t* rows = nullptr);
     bool pipe_ran = false;  // the last run used the pipelined kernel
     // opt-in time-parallel scores (segments of >= seg observations, probes of `probe`; see
     // runtime.cpp); synchronous; *fallbacks = segments that did not converge within the probe

@@ -286,6 +286,13 @@ int svh_batch_step_floor_ms(svh_batch_t b, void* stream, uint32_t reps, float* m
     });
 }
 
+int svh_batch_fallback_rows(svh_batch_t b, uint32_t* flags) {
+    return guarded([&] {
+        require(b && flags, "null argument");
+        (void)b->impl->pipe_fallbacks(flags);
+    });
+}
+
 int svh_batch_fallbacks(svh_batch_t b, uint64_t* rows) {
     return guarded([&] {
         require(b && rows, "null argument");

@@ -20,6 +20,7 @@ _u64 = ctypes.POINTER(ctypes.c_uint64)
 _f32 = ctypes.POINTER(ctypes.c_float)
 _i64 = ctypes.POINTER(ctypes.c_int64)
 _i32 = ctypes.POINTER(ctypes.c_int32)
+_u32 = ctypes.POINTER(ctypes.c_uint32)
 
 
 def _p(a, t):
@@ -216,6 +217,13 @@ class DeviceBatch:
         r = ctypes.c_uint64()
         _lib.check(_lib.lib.svh_batch_fallbacks(self._h, ctypes.byref(r)))
         return int(r.value)
+
+    def fallback_rows(self) -> np.ndarray:
+        """Per row (svh_batch_fallback_rows): bit 0 the step pass re-ran it exactly, bit 1 the
+        level-2 pipelined pass handed it to the on-chip chunk kernel."""
+        f = np.zeros(self.nseq, np.uint32)
+        _lib.check(_lib.lib.svh_batch_fallback_rows(self._h, _p(f, _u32)))
+        return f
 
     def debug_fault(self, stream: int | None = None) -> None:
         """Diagnostics (svh_batch_debug_fault): mark the last run as if a bounded wait had given
