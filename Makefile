@@ -18,7 +18,7 @@ HOSTFLAGS := --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wa
 
 HIP_SRCS  := $(wildcard $(CSRC)/fused_*.hip) $(CSRC)/misc.hip $(CSRC)/band.hip $(wildcard $(CSRC)/chain_*.hip) $(CSRC)/timepar.hip $(CSRC)/pipe.hip \
              $(CSRC)/pipe_tm1.hip $(CSRC)/pipe_tm1p.hip $(CSRC)/pipe_wide.hip $(CSRC)/pipe_wide_paths.hip $(CSRC)/pipe_paths.hip \
-             $(CSRC)/spec2.hip $(CSRC)/pipe_l2.hip
+             $(CSRC)/spec2.hip $(CSRC)/pipe_l2.hip $(CSRC)/diag.hip
 HOST_SRCS := $(CSRC)/runtime.cpp $(CSRC)/svh_api.cpp $(CSRC)/HIP_impl.cpp $(CSRC)/data_reader.cpp $(CSRC)/stream.cpp \
              $(CSRC)/seqreader.cpp $(CSRC)/chunker.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS))

@@ -43,7 +43,8 @@ DATA = os.path.join(ROOT, "data")
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_GHZ = 2.4         # MI355X_MICROARCH.md: max shader clock
-KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain", 5: "pipe", 6: "pipew", 7: "spec2", 8: "spec2-pipe"}
+KERNEL_NAMES = {1: "fused", 2: "generic", 3: "band", 4: "chain", 5: "pipe", 6: "pipew", 7: "spec2", 8: "spec2-pipe",
+                9: "diag"}
 
 
 def parse(argv=None):
@@ -293,8 +294,12 @@ def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc, essential_bytes) -> d
     wide = plan["threads"] == info.get("wide_threads") and plan["slots"] == info.get("wide_slots") and nseq > info["cu_count"]
     wg_per_cu = 4 if wide else 1  # launch-bounds occupancy of the wide plan; one WG per CU otherwise
     pipew = plan["kernel"] == 6
+    diag = plan["kernel"] == 9
     wgs = nseq * int(info.get("pipe_groups", 1)) if pipe else nseq
     if pipe:
+        wg_per_cu = max(1, -(-wgs // max(info["cu_count"], 1)))
+    if diag:  # ceil(nseq / W) groups x diag_ranges workgroups of W waves, spread evenly over the CUs
+        wgs = -(-nseq // waves_per_wg) * int(info.get("diag_ranges", 1))
         wg_per_cu = max(1, -(-wgs // max(info["cu_count"], 1)))
     if pipew:
         wgs = -(-nseq // waves_per_wg) * int(info.get("pipew_blocks", 1))
@@ -574,14 +579,14 @@ def main(argv=None):
                  else "spec_chunk+" + KERNEL_NAMES.get(plan["kernel"], "?") if args.level >= 2
                  else KERNEL_NAMES.get(plan["kernel"], "?"))
         pmc = None
-        if not args.no_pmc and world == 1 and (args.level <= 1 or spec2 or l2pipe) and plan["kernel"] in (4, 5, 6, 7, 8):
+        if not args.no_pmc and world == 1 and (args.level <= 1 or spec2 or l2pipe) and plan["kernel"] in (4, 5, 6, 7, 8, 9):
             # the dominant kernel's counters (with --paths: the pipelined kernel's PATHS variant, the
             # pass's dominant kernel; its traceback and the exiting chain launch are not counted;
             # level 2: the on-chip chunk kernel, not the step kernels' one-observation tails)
             largs = ["--model", args.model, "--ess", ess_name, "--replicate", str(args.replicate), "--steps", "3",
                      "--warmup", "1", "--level", str(args.level)] + (["--paths"] if args.paths else [])
             kpref = {4: "chain_viterbi_kernel", 5: "pipe_viterbi_kernel", 6: "pipew_viterbi_kernel",
-                     7: "spec2_kernel", 8: "pipe_viterbi_kernel"}[plan["kernel"]]
+                     7: "spec2_kernel", 8: "pipe_viterbi_kernel", 9: "diag_viterbi_kernel"}[plan["kernel"]]
             # level 2 on the pipelined plan: its L2 instantiation (template argument L2 = true), not the
             # step kernel's one-observation tails that share the name
             pmc = pmc_counters(largs, "void svh::(anonymous namespace)::" + kpref, ", true>" if l2pipe else "")

@@ -30,8 +30,9 @@
 extern "C" {
 #endif
 
-#define SVH_ABI_VERSION 3  /* 2: svh_model_info pipe_* fields, SVH_KERNEL_PIPE, svh_batch_fallbacks;
-                              3: pipe_max_nseq_paths, SVH_KERNEL_SPEC2_PIPE, SVH_BATCH_NO_TIMING */
+#define SVH_ABI_VERSION 4  /* 2: svh_model_info pipe_* fields, SVH_KERNEL_PIPE, svh_batch_fallbacks;
+                              3: pipe_max_nseq_paths, SVH_KERNEL_SPEC2_PIPE, SVH_BATCH_NO_TIMING;
+                              4: SVH_KERNEL_DIAG, svh_model_info diag_* fields */
 
 enum {
     SVH_OK = 0,
@@ -73,7 +74,7 @@ void svh_ess_free(svh_ess_t e);
  * the fused (or generic) kernel with 16-bit backpointers. */
 enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2, SVH_KERNEL_BAND = 3,
        SVH_KERNEL_CHAIN = 4, SVH_KERNEL_PIPE = 5, SVH_KERNEL_PIPE_WIDE = 6, SVH_KERNEL_SPEC2 = 7,
-       SVH_KERNEL_SPEC2_PIPE = 8 };
+       SVH_KERNEL_SPEC2_PIPE = 8, SVH_KERNEL_DIAG = 9 };
 /* PIPE: the pipelined chain kernel (MSV-shaped models whose feeder row N takes terms only from
  * the light rows and itself): a sequence's states are split over many waves and CUs; N's light
  * term is speculated away and checked exactly at every observation, and a sequence that fails
@@ -89,7 +90,12 @@ enum { SVH_KERNEL_AUTO = 0, SVH_KERNEL_FUSED = 1, SVH_KERNEL_GENERIC = 2, SVH_KE
  * SPEC2_PIPE (reported by svh_batch_plan only): _spec level 2 on the pipelined latency plan
  * (pipe_l2.hip: every chunk of every row in one launch, the light term of N and its two-hop terms
  * speculated away and checked exactly, flagged rows re-run by spec2.hip); AUTO and PIPE use it for
- * MSV-shaped models whose scores are all >= 0. */
+ * MSV-shaped models whose scores are all >= 0.
+ * DIAG: the pipelined plan's recurrence with every lane on an anti-diagonal of the (state,
+ * observation) grid: a state's chain input is the lane's own previous score, so no wave waits for
+ * another (diag.hip).  Scores-only passes from the first observation; AUTO uses it for the batches
+ * the latency plan used to take (svh_model_info.diag_max_nseq); selecting it runs every scores-only
+ * pass of the model on it (decoded paths and the _spec tail use the chain kernel). */
 
 typedef struct {
     int32_t device;      /* HIP device ordinal; -1 = the caller's current device */
@@ -142,6 +148,8 @@ typedef struct {
     uint32_t pipe_max_nseq_paths; /* ... the latency plan's bound for decoded-path batches (one
                                      workgroup per CU; pipe_max_nseq allows two for scores; the
                                      SVH_PIPE_MAX_NSEQ override applies to scores only) */
+    int32_t diag_ranges;   /* diagonal plan (SVH_KERNEL_DIAG): ranges of 64 diagonals per sequence, 0 = none */
+    uint32_t diag_max_nseq; /* AUTO runs it for scores-only batches of at most this many sequences */
 } svh_model_info;
 /* The model's plan for a one-sequence scores-only run (kernel/threads/slots describe it). */
 int svh_model_get_info(svh_model_t m, svh_model_info* info);

@@ -34,6 +34,7 @@ SVH_KERNEL_PIPE = 5
 SVH_KERNEL_PIPE_WIDE = 6
 SVH_KERNEL_SPEC2 = 7  # svh_batch_plan only: _spec level 2 on chip
 SVH_KERNEL_SPEC2_PIPE = 8  # svh_batch_plan only: _spec level 2 on the pipelined latency plan
+SVH_KERNEL_DIAG = 9  # the diagonal plan (diag.hip): scores-only passes, no inter-wave exchange
 SVH_BATCH_PATHS = 1
 SVH_BATCH_NO_TIMING = 2  # no start/stop events per run (svh_batch_elapsed_ms unavailable)
 SVH_MODEL_SPEC_DENSE = 1
@@ -61,6 +62,8 @@ class svh_model_info(ctypes.Structure):
         ("pipe_groups", c_int32), ("pipe_max_nseq", c_uint32),
         ("pipew_slots", c_int32), ("pipew_waves", c_int32), ("pipew_blocks", c_int32), ("pipew_min_nseq", c_uint32),
         ("pipe_max_nseq_paths", c_uint32),
+        ("diag_ranges", c_int32),
+        ("diag_max_nseq", c_uint32),
     ]
 
 

@@ -212,6 +212,10 @@ struct PipeModel {
     uint32_t wide;          // 1: the wide plan's geometry and table layout (pipe_wide_kernel.h)
     float emax2;            // _spec level 2 on this plan (pipe_l2.hip): the largest finite ea over
                             // positions and symbols (its margin check), +inf: level 2 not supported
+    // diagonal plan (diag.hip): the table [S][64 nrng] float2 {ea_p(o), eb_p(o)} of positions 0 .. 64 nrng - 1
+    // in chain order (+inf past the light rows), nrng ranges of 64 diagonals per sequence; null: no plan
+    const float2* dtab;
+    uint32_t nrng;
     uint32_t rerun;         // latency plan, scores: a row whose speculation fails is re-run exactly by
                             // its combining workgroup (pipe_rerun_row; needs 2P + 2W floats of the ring's
                             // LDS), so no fallback launch follows the pass; 0: the host launches one
@@ -298,6 +302,15 @@ constexpr uint32_t kPRingStride = 132;  // floats per row: 64 lanes x 2 + 4 padd
 constexpr uint32_t kPPlane = 260;       // floats: 64 x 4 + 4 (260 = 4 mod 64)
 constexpr uint32_t kPQuadStride = 520;  // floats: two planes (520 = 8 mod 64)
 inline size_t pipe_path_lds_bytes(uint32_t W) { return (size_t)W * 8 * kPQuadStride * 4; }
+// Diagonal plan (diag.hip): the latency plan's recurrence with every lane on an anti-diagonal of the
+// (position, observation) grid -- lane l of range r holds position (64 r + l + i) mod (64 nrng) after
+// step i, so a position's chain input is the lane's own previous score (no exchange between waves).
+// A workgroup is diag_waves_for(nseq) sequences x one range; rows whose speculation fails are re-run
+// in the same launch.  Scores only, rows from observation 0 (b.v_in null).
+uint32_t diag_waves_for(uint64_t nseq);
+size_t diag_lds_bytes(uint32_t W, uint32_t S, uint32_t P);
+hipError_t launch_diag(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);
+
 // Wide pipelined plan (pipe_wide.hip): one block of 64*SM positions per workgroup, W sequences
 // (one per wave), the block's table [nblk][S][NC][64] float4 in LDS (PipeModel.tab; G = nblk);
 // NC = SM/2 (eb|ea) chunks + {A_S A_F X_SS X_FF} [+ {X_SF 0 0 0} when sx], constants per lane.

@@ -23,6 +23,16 @@ __device__ __forceinline__ void g_st64(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A score that a re-run on another XCD may overwrite in the same launch (the in-kernel re-run of a
+// row whose speculation failed): an agent-scope store, written through to memory, not left dirty in
+// this XCD's L2 -- the L2s are not coherent, and a dirty line written back after the re-run's stores
+// would put the speculated value back (measured: rows re-run from another XCD came out wrong
+// intermittently on the diagonal plan, tools/diag_stress.py).
+__device__ __forceinline__ void g_st_score(float* p, float v) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ float readlane_f(float x, uint32_t l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), (int)l));
 }

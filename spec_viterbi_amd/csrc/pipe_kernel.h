@@ -1571,7 +1571,8 @@ __global__ __launch_bounds__(64 * W) void pipe_viterbi_kernel(PipeModel m, Fused
         for (int s = 0; s < SM; ++s) {
             const uint32_t r = m.lrow[p0 + s];
             if (r != kNoRow) {
-                out[r] = v[s];
+                if (PATHS || L2) out[r] = v[s];
+                else g_st_score(out + r, v[s]);  // the row's re-run may come from another XCD
                 lex_min(bvv, bk, v[s], r);
             }
         }

@@ -699,6 +699,25 @@ PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm, uint32_t waves, bool w
             }
         }
     }
+    // diagonal plan (diag.hip): position-major planes {ea, eb} per symbol over 64 nrng positions (the
+    // light rows in chain order, then +inf dummies); position 0 has no chain term (bw_0 = +inf), which
+    // the diagonals rely on when they wrap
+    if (!wide && sm == 2) {
+        pp.nrng = (nL + 63) / 64;
+        const uint32_t NP = pp.nrng * 64;
+        pp.dtab.assign((size_t)S * NP * 2, kInfH);
+        for (uint32_t p = 0; p < nL; ++p)
+            for (uint32_t o = 0; o < S; ++o) {
+                const float e = hm.emis[(size_t)o * n + sh.light[p]];
+                float* d = pp.dtab.data() + ((size_t)o * NP + p) * 2;
+                d[0] = e + sh.aw[0][p];
+                d[1] = e + sh.bw[p];
+            }
+        if (sh.bw[0] < kInfH) {  // cannot happen (analyze_band: p > 0), but the wrap depends on it
+            pp.nrng = 0;
+            pp.dtab.clear();
+        }
+    }
     // decoded paths: term flags per position (as BandPlan::pflags with heavy feeder F) and the
     // state -> position map (-1 F, -2 S)
     pp.pflags.assign(P, 0);
@@ -793,6 +812,11 @@ void DevicePipePlan::upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream
     view.sx = p.sx ? 1u : 0u;
     view.wide = p.wide ? 1u : 0u;
     view.rerun = !p.wide && pipe_rerun_fits(p.P, p.W) ? 1u : 0u;
+    if (p.nrng && !p.dtab.empty() && diag_lds_bytes(diag_waves_for(4), S, p.P) <= 160 * 1024) {
+        d_dtab.upload(p.dtab.data(), p.dtab.size() * 4, s);
+        view.dtab = d_dtab.as<float2>();
+        view.nrng = p.nrng;
+    }
     view.emax2 = p.emax2;
     // the pair-table step wherever it applies: TM = 4 (indexed operands, packed feeder terms:
     // 0.255 ms on the headline against 0.263 / 0.268 / 0.277 for TM 2 / 3 / 1 and 0.334 for the
@@ -1004,8 +1028,8 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
     if (dev < 0) hip_check(hipGetDevice(&dev), "hipGetDevice");
     device = dev;
     kernel_pref = opts ? opts->kernel : SVH_KERNEL_AUTO;
-    if (kernel_pref < SVH_KERNEL_AUTO || kernel_pref > SVH_KERNEL_PIPE_WIDE)
-        throw Error(SVH_E_INVALID, "kernel must be one of SVH_KERNEL_AUTO .. SVH_KERNEL_PIPE_WIDE");
+    if (kernel_pref < SVH_KERNEL_AUTO || (kernel_pref > SVH_KERNEL_PIPE_WIDE && kernel_pref != SVH_KERNEL_DIAG))
+        throw Error(SVH_E_INVALID, "kernel must be one of SVH_KERNEL_AUTO .. SVH_KERNEL_PIPE_WIDE or SVH_KERNEL_DIAG");
     if (opts && (opts->flags & ~SVH_MODEL_SPEC_DENSE))
         throw Error(SVH_E_INVALID, "unknown svh_model_opts.flags bits");
     spec_dense = opts && (opts->flags & SVH_MODEL_SPEC_DENSE);
@@ -1018,7 +1042,7 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
     hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
 
     if (kernel_pref == SVH_KERNEL_AUTO || kernel_pref == SVH_KERNEL_BAND || kernel_pref == SVH_KERNEL_CHAIN ||
-        kernel_pref == SVH_KERNEL_PIPE || kernel_pref == SVH_KERNEL_PIPE_WIDE) {
+        kernel_pref == SVH_KERNEL_PIPE || kernel_pref == SVH_KERNEL_PIPE_WIDE || kernel_pref == SVH_KERNEL_DIAG) {
         BandPlan bpl;
         if (kernel_pref != SVH_KERNEL_BAND) bpl = make_band_plan(host, max_threads, true);
         if (!bpl.ok && kernel_pref != SVH_KERNEL_CHAIN) bpl = make_band_plan(host, max_threads, false);
@@ -1040,7 +1064,8 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
                 pipe_wide.view.cus = (uint32_t)cus;
             }
         }
-        if ((kernel_pref == SVH_KERNEL_PIPE && !pipe.plan.ok) || (kernel_pref == SVH_KERNEL_PIPE_WIDE && !pipe_wide.plan.ok))
+        if (((kernel_pref == SVH_KERNEL_PIPE || kernel_pref == SVH_KERNEL_DIAG) && !pipe.plan.ok) ||
+            (kernel_pref == SVH_KERNEL_DIAG && !pipe.view.dtab) || (kernel_pref == SVH_KERNEL_PIPE_WIDE && !pipe_wide.plan.ok))
             throw Error(SVH_E_UNSUPPORTED, "pipelined kernel requested but the model does not qualify (chain shape "
                                            "with one heavy row feeding the light rows, emit_num <= 32)");
         band.upload(bpl, host.n, host.S, stream);
@@ -1065,6 +1090,12 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
             pipe_max_nseq = std::max<uint32_t>(1, 2 * cu_count / pipe.plan.G);
             pipe_max_nseq_paths = std::max<uint32_t>(1, cu_count / pipe.plan.G);
             if (const char* e = std::getenv("SVH_PIPE_MAX_NSEQ")) pipe_max_nseq = (uint32_t)std::atoi(e);
+            // diagonal plan (diag.hip): the scores-only batches the latency plan would take (DESIGN.md
+            // 5l); SVH_DIAG=0 disables it, SVH_DIAG_MAX_NSEQ overrides the bound
+            if (pipe.view.dtab && !(std::getenv("SVH_DIAG") && std::atoi(std::getenv("SVH_DIAG")) == 0)) {
+                diag_max_nseq = pipe_max_nseq;
+                if (const char* e = std::getenv("SVH_DIAG_MAX_NSEQ")) diag_max_nseq = (uint32_t)std::atoi(e);
+            }
         }
         if (pipe_wide.plan.ok) {
             // AUTO: the wide pipelined plan for batches beyond the latency plan's range
@@ -1130,7 +1161,8 @@ CsrModel Model::csr_view() const {
 const DeviceBandPlan* Model::band_for(bool paths, uint32_t nseq) const {
     if (!band.plan.ok) return nullptr;
     if (kernel_pref != SVH_KERNEL_AUTO && kernel_pref != SVH_KERNEL_BAND && kernel_pref != SVH_KERNEL_CHAIN &&
-        kernel_pref != SVH_KERNEL_PIPE && kernel_pref != SVH_KERNEL_PIPE_WIDE)  // PIPE*: the chain plan is its fallback
+        kernel_pref != SVH_KERNEL_PIPE && kernel_pref != SVH_KERNEL_PIPE_WIDE && kernel_pref != SVH_KERNEL_DIAG)
+        // PIPE*, DIAG: the chain plan is their fallback (paths, the _spec tail)
         return nullptr;
     if (paths) return band.plan.paths_ok() ? &band : nullptr;  // decoded-path chain variant
     if (band_wide.plan.ok && nseq > cu_count) return &band_wide;
@@ -1144,6 +1176,13 @@ const DevicePipePlan* Model::pipe_for(uint32_t nseq) const {
     if (pipe.plan.ok && nseq <= pipe_max_nseq) return &pipe;
     if (pipe_wide.plan.ok && nseq >= pipew_min_nseq) return &pipe_wide;
     return nullptr;
+}
+
+const DevicePipePlan* Model::diag_for(uint32_t nseq) const {
+    if (!pipe.plan.ok || !pipe.view.dtab) return nullptr;
+    if (kernel_pref == SVH_KERNEL_DIAG) return &pipe;
+    if (kernel_pref != SVH_KERNEL_AUTO) return nullptr;
+    return nseq <= diag_max_nseq ? &pipe : nullptr;
 }
 
 // Decoded paths: the latency plan's path variant for the batches its scores pass takes, the wide
@@ -1472,6 +1511,17 @@ svh_model_info Model::info(uint32_t nseq, bool paths, uint32_t level) const {
         i.pipe_max_nseq = kernel_pref == SVH_KERNEL_PIPE ? 0xFFFFFFFFu : pipe_max_nseq;
         i.pipe_max_nseq_paths = kernel_pref == SVH_KERNEL_PIPE ? 0xFFFFFFFFu : pipe_max_nseq_paths;
     }
+    if (!paths && steps && level <= 1 && nseq && diag_for(nseq)) {  // scores on the diagonal plan
+        const uint32_t w = diag_waves_for(nseq);
+        i.kernel = SVH_KERNEL_DIAG;
+        i.threads = (int32_t)(64 * w);
+        i.slots = 1;
+        i.lds_bytes = diag_lds_bytes(w, host.S, pipe.plan.P);
+    }
+    if (pipe.view.dtab) {
+        i.diag_ranges = (int32_t)pipe.plan.nrng;
+        i.diag_max_nseq = kernel_pref == SVH_KERNEL_DIAG ? 0xFFFFFFFFu : kernel_pref == SVH_KERNEL_AUTO ? diag_max_nseq : 0u;
+    }
     if (level == 2 && spec_level == 2 && nseq && pipe_l2_on()) {  // the chunks on the pipelined plan
         i.kernel = SVH_KERNEL_SPEC2_PIPE;
         i.threads = (int32_t)(64 * pipe.plan.W);
@@ -1759,7 +1809,11 @@ void Batch::run(uint32_t level, hipStream_t s) {
     }
     pipe_ran = false;
     l2_ran = false;
-    if (const DevicePipePlan* pp = paths ? nullptr : model->pipe_for(nseq)) {  // pipelined plan: scratch
+    if (const DevicePipePlan* dp = paths || level >= 2 ? nullptr : model->diag_for(nseq)) {  // diagonal plan: scratch
+        pipe.ensure(nseq, dp->plan.nrng, s);
+        fb.pipe = &pipe.view;
+        pipe_ran = true;
+    } else if (const DevicePipePlan* pp = paths ? nullptr : model->pipe_for(nseq)) {  // pipelined plan: scratch
         pipe.ensure(nseq, pp->plan.G, s);
         pipe.note_launch(s);
         fb.pipe = &pipe.view;
@@ -2220,6 +2274,12 @@ void Batch::read_async(hipStream_t s, float* scores, int64_t* best, int32_t* pat
 void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) const {
     const DevicePlan* dp = plan_for(want_paths);
     const DeviceBandPlan* bpl = band_for(want_paths, b.nseq);
+    const DevicePipePlan* dpl = want_paths || b.v_in ? nullptr : diag_for(b.nseq);
+    if (dpl && b.pipe && b.pipe->rows >= b.nseq && b.pipe->G >= dpl->plan.nrng) {
+        // diagonal plan: rows whose speculation fails are re-run in the same launch
+        hip_check(launch_diag(dpl->view, b, *b.pipe, s), "diagonal Viterbi kernel");
+        return;
+    }
     const DevicePipePlan* ppl = want_paths ? nullptr : pipe_for(b.nseq);
     if (ppl && bpl && b.pipe && b.pipe->rows >= b.nseq && b.pipe->G >= ppl->plan.G) {
         if (ppl->plan.wide) hip_check(launch_pipew(ppl->view, b, *b.pipe, s), "wide pipelined Viterbi kernel");

@@ -139,6 +139,9 @@ struct PipePlan {
     std::vector<uint32_t> lrow; // [P]
     std::vector<float> hc;      // [S][8]
     bool wide = false;          // pipe_wide.hip layout: tab [nblk][S][SM/2][64][4], W sequences per workgroup
+    // diagonal plan (diag.hip; latency plan only): [S][64 nrng] float2 {ea, eb}, +inf past the light rows
+    std::vector<float> dtab;
+    uint32_t nrng = 0;
     // _spec level 2 on this plan (pipe_l2.hip): the largest finite ea = fl(E_o[p] + aw_p), or +inf
     // when some score is negative (its margin check needs every score >= 0) or the plan is wide
     float emax2 = 0.0f;
@@ -153,7 +156,7 @@ PipePlan make_pipe_plan(const HostModel& hm, uint32_t sm = 0, uint32_t waves = 0
 
 struct DevicePipePlan {
     PipePlan plan;
-    DeviceBuffer d_tab, d_e0, d_start, d_lrow, d_hc, d_stamps, d_pflags, d_spos;
+    DeviceBuffer d_tab, d_e0, d_start, d_lrow, d_hc, d_stamps, d_pflags, d_spos, d_dtab;
     PipeModel view{};
     void upload(const PipePlan& p, uint32_t n, uint32_t S, hipStream_t s);
     void report_stamps(uint32_t nseq) const;  // diagnostic (SVH_PIPE_DEBUG): first sequence's waves
@@ -228,6 +231,9 @@ struct Model {
     DevicePipePlan pipe;             // pipelined chain plan (latency path for small batches)
     uint32_t pipe_max_nseq = 0;      // AUTO: pipelined plan for scores-only batches of at most this many rows
     uint32_t pipe_max_nseq_paths = 0;  // ... for decoded-path batches
+    uint32_t diag_max_nseq = 0;      // AUTO: the diagonal plan (diag.hip) for scores-only batches of at most this many rows
+    // diagonal plan for a scores-only pass over nseq rows from observation 0 (nullptr: none)
+    const DevicePipePlan* diag_for(uint32_t nseq) const;
     DevicePipePlan pipe_wide;        // wide pipelined plan (throughput path for batches that fill the chip)
     uint32_t pipew_min_nseq = 0;     // AUTO: wide pipelined plan for batches of at least this many rows
     DevicePlan fast_plan;            // fastest fused plan (may use uniform heavy rows)

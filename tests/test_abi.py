@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_error_channel():
-    assert L.lib.svh_abi_version() == 3
+    assert L.lib.svh_abi_version() == 4
     h = ctypes.c_void_p()
     rc = L.lib.svh_hmm_read(b"/nonexistent.chmm", ctypes.byref(h))
     assert rc == L.SVH_E_IO

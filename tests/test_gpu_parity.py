@@ -83,8 +83,8 @@ def test_2405_emit50_full_batch_vs_oracle():
     model = svh.DeviceModel(hmm)
     batch = model.batch(seqs)
     plan = batch.plan()
-    # AUTO takes the pipelined latency plan for this batch (50 sequences x 5 workgroups)
-    assert plan["kernel"] == _lib.SVH_KERNEL_PIPE and plan["pipe_groups"] == 5, plan
+    # AUTO takes the diagonal plan for this batch (13 groups of 4 sequences x 38 ranges)
+    assert plan["kernel"] == _lib.SVH_KERNEL_DIAG and plan["diag_ranges"] == 38, plan
     batch.run()
     scores, best = batch.read()
     assert batch.fallbacks() == 0

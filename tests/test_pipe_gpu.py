@@ -85,7 +85,10 @@ def test_pipe_auto_selects_pipe_for_small_batches():
     info = model.info()
     assert info["pipe_slots"] > 0 and info["pipe_groups"] > 1
     small = model.batch(random_seqs(20, [50] * 4, seed=1))
-    assert small.plan()["kernel"] == _lib.SVH_KERNEL_PIPE
+    assert small.plan()["kernel"] == _lib.SVH_KERNEL_DIAG  # the latency plan's range: the diagonal plan
+    assert info["diag_max_nseq"] == info["pipe_max_nseq"], info
+    forced = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_PIPE).batch(random_seqs(20, [50] * 4, seed=1))
+    assert forced.plan()["kernel"] == _lib.SVH_KERNEL_PIPE
     wide = model.batch(random_seqs(20, [8] * (info["pipe_max_nseq"] + 1), seed=2))
     assert info["pipew_min_nseq"] == info["pipe_max_nseq"] + 1 and info["pipew_blocks"] == 5, info
     assert wide.plan()["kernel"] == _lib.SVH_KERNEL_PIPE_WIDE
@@ -115,11 +118,12 @@ def test_pipe_auto_two_workgroups_per_cu(name, ess_name, nseq):
             for q in range(nseq)]
     if name == "100.chmm":  # 400 x 3500 x 101 states through the oracle: shorter rows keep it quick
         seqs = [s[: 1200 + 7 * q] for q, s in enumerate(seqs)]
-    model = svh.DeviceModel(hmm)
-    info = model.info()
+    info = svh.DeviceModel(hmm).info()
     G = info["pipe_groups"]
     assert info["pipe_max_nseq"] == 2 * info["cu_count"] // G, info
     assert info["cu_count"] < nseq * G <= 2 * info["cu_count"], (nseq, G, info["cu_count"])
+    # AUTO runs these batches on the diagonal plan (test_diag_gpu.py); the latency plan forced
+    model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_PIPE)
     batch = model.batch(seqs)
     assert batch.plan()["kernel"] == _lib.SVH_KERNEL_PIPE
     batch.run()

@@ -114,7 +114,7 @@ def test_two_headline_batches_on_two_streams():
     hmm = svh.read_HMM(chmm("2405.chmm"))
     seqs = svh.read_emit_seq(ess("emit_50_3500_20.ess"))
     ref = load_digests()["2405.chmm x emit_50_3500_20.ess"]
-    model = svh.DeviceModel(hmm)
+    model = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_PIPE)  # (AUTO: the diagonal plan, test_diag_gpu.py)
     a, b = model.batch(seqs), model.batch(seqs)
     assert a.plan()["kernel"] == _lib.SVH_KERNEL_PIPE and a.plan()["pipe_groups"] == 5
     sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
