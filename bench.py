@@ -279,7 +279,7 @@ def spec2_essential_bytes(n: int, S: int, lengths, table_bytes: int, xcds: int =
     return sum(lengths) + nseq * n * 4 + nseq * 8 + xcds * (table_bytes + S * n * 4)
 
 
-def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc, essential_bytes) -> dict:
+def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc, essential_bytes, steps=0) -> dict:
     """VALU-issue roofline of the step kernels (the per-observation step is VALU + LDS work on
     registers; HBM carries only symbols in and scores out).  Capacity of one SIMD-32: one wave64
     VALU instruction per 2 cycles, and at most one per 4 cycles from a single wave
@@ -355,6 +355,21 @@ def roofline(info, plan, nseq, kernel_ms, algo_bytes, pmc, essential_bytes) -> d
                           "addr_conflict_per_active": round(pmc.get("SQ_LDS_ADDR_CONFLICT", 0) / max(pmc.get("SQ_ACTIVE_INST_LDS", 1), 1), 4)}
         if "GRBM_GUI_ACTIVE" in pmc:
             res["profiled_clock_ghz"] = round(pmc["GRBM_GUI_ACTIVE"] / 8 / (kernel_ms * 1e6), 3)
+        if diag and "SQ_INSTS_SALU" in pmc and "SQ_INSTS_LDS" in pmc and "SQ_WAVES" in pmc and steps:
+            # the diagonal plan has no exchange: its bound is instruction issue on the SIMDs it
+            # occupies. Per wave and step: instructions of each kind; per SIMD: the
+            # cycles one instruction took on average (every SIMD holding waves_per_simd waves)
+            allins = pmc["SQ_INSTS_VALU"] + pmc["SQ_INSTS_SALU"] + pmc["SQ_INSTS_LDS"]
+            waves = max(pmc["SQ_WAVES"], 1)
+            clk = res.get("profiled_clock_ghz") or CLOCK_GHZ
+            simds = cus * 4
+            res["issue"] = {"valu_per_step": round(pmc["SQ_INSTS_VALU"] / waves / steps, 2),
+                            "salu_per_step": round(pmc["SQ_INSTS_SALU"] / waves / steps, 2),
+                            "lds_per_step": round(pmc["SQ_INSTS_LDS"] / waves / steps, 2),
+                            "instr_per_step": round(allins / waves / steps, 2),
+                            "simd_cycles_per_instr": round(kernel_ms * 1e6 * clk * simds / allins, 2),
+                            "note": "per wave and observation step (steps = the longest row's observations - 1); "
+                                    "simd_cycles_per_instr = kernel cycles x occupied SIMDs / instructions issued"}
     if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:  # KiB; FETCH_SIZE doubled on gfx950
         traffic = 2.0 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024
         res["traffic"] = round(traffic)
@@ -598,7 +613,7 @@ def main(argv=None):
             ess_b = essential_bytes_per_launch(n, int(info["S"]), lengths, False)
         else:
             ess_b = algo if args.level >= 2 else essential_bytes_per_launch(n, int(info["S"]), lengths, args.paths)
-        rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc, ess_b)
+        rl = roofline(info, plan, len(seqs), kernel_ms, algo, pmc, ess_b, max(lengths) - 1)
         floor_ms = None
         if plan["kernel"] == 5 and not args.paths and args.level <= 1 and batch:
             # the latency plan's own floor, measured live: the same launch with every boundary exchange
@@ -641,7 +656,8 @@ def main(argv=None):
                 "observations_per_gpu": sum(lengths), "state_updates_per_gpu": updates_per_rank, "level": args.level,
                 "kernel": kname, "threads": plan["threads"], "slots": plan["slots"], "paths": bool(args.paths),
                 "workgroups_per_sequence": (int(info["pipe_groups"]) if plan["kernel"] == 5 else
-                                            int(info["pipew_blocks"]) if plan["kernel"] == 6 else 1),
+                                            int(info["pipew_blocks"]) if plan["kernel"] == 6 else
+                                            int(info["diag_ranges"]) if plan["kernel"] == 9 else 1),
                 "fallback_rows": fallbacks,
                 "heavy_rows": plan["heavy_rows"], "spec_prep_s": None if prep_s is None else round(prep_s, 4),
                 "golden_checked": golden_checked,

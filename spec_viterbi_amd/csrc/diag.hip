@@ -48,10 +48,15 @@ namespace svh {
 
 namespace {
 
-constexpr uint32_t kDR = 160;         // ring columns (five groups of kDK)
+#ifndef SVH_DIAG_K
+#define SVH_DIAG_K 64
+#endif
+constexpr uint32_t kDK = SVH_DIAG_K;  // steps per block (= columns per ring group; 32 or 64)
+static_assert(kDK == 32 || kDK == 64, "block length");
+constexpr uint32_t kDR = 5 * kDK;     // ring columns (five groups of kDK)
 constexpr uint32_t kDRS = kDR + 64;   // slots per symbol plane: the ring and a mirror of its first 64
-constexpr uint32_t kDG = kDR / 32;    // ring groups
-constexpr uint32_t kDK = 32;          // steps per block (= columns per ring group)
+constexpr uint32_t kDG = kDR / kDK;   // ring groups
+constexpr uint32_t kCP = kDK / 2;     // 16-byte chunks of a plane's group (two columns each)
 constexpr uint32_t kDE = 8;           // floats per stream entry
 #ifndef SVH_DIAG_PS
 #define SVH_DIAG_PS 6
@@ -126,11 +131,11 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
         rrow[w] = kNoRow;
     }
 
-    // ---- ring refill: group g = columns u in [32 g, 32 g + 32) of this range (table column
+    // ---- ring refill: group g = columns u in [kDK g, kDK g + kDK) of this range (table column
     // (64 rg + u) mod NP), every symbol plane; 16 chunks of 16 bytes per plane over the workgroup
     constexpr uint32_t kT = 64 * W;
-    constexpr uint32_t kRep = (16 * kDMaxSym + kT - 1) / kT;
-    const uint32_t nchunk = 16 * S;
+    constexpr uint32_t kRep = (kCP * kDMaxSym + kT - 1) / kT;
+    const uint32_t nchunk = kCP * S;
     typedef float lvec __attribute__((ext_vector_type(4 * kRep)));  // a vector, not an array: stays in VGPRs
     lvec lreg;
     auto gload = [&](uint32_t g) {
@@ -139,7 +144,7 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
         for (uint32_t r = 0; r < kRep; ++r) {
             // unconditional (clamped) loads: the registers stay registers
             const uint32_t k = min(tid + r * kT, nchunk - 1);
-            const float4 v = *reinterpret_cast<const float4*>(m.dtab + (size_t)(k >> 4) * NP + c0 + 2 * (k & 15u));
+            const float4 v = *reinterpret_cast<const float4*>(m.dtab + (size_t)(k / kCP) * NP + c0 + 2 * (k % kCP));
             lreg[4 * r] = v.x;
             lreg[4 * r + 1] = v.y;
             lreg[4 * r + 2] = v.z;
@@ -152,7 +157,7 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
         for (uint32_t r = 0; r < kRep; ++r) {
             const uint32_t k = tid + r * kT;
             if (k < nchunk) {
-                float* d = ring + ((size_t)(k >> 4) * kDRS + s0 + 2 * (k & 15u)) * 2;
+                float* d = ring + ((size_t)(k / kCP) * kDRS + s0 + 2 * (k % kCP)) * 2;
                 const float4 v = make_float4(lreg[4 * r], lreg[4 * r + 1], lreg[4 * r + 2], lreg[4 * r + 3]);
                 *reinterpret_cast<float4*>(d) = v;
                 if (s0 < 64) *reinterpret_cast<float4*>(d + kDR * 2) = v;
@@ -265,6 +270,12 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
 #ifndef SVH_DIAG_AB
 #define SVH_DIAG_AB 0
 #endif
+    auto blockwork = [&](uint32_t kb) {
+        lwrite(kb + 4);  // into the slots of group kb - 1, which no wave reads any more
+        gload(kb + 5);
+        sbuild(kb + 1);  // into the buffer of block kb - 1 (the last steps of block kb read its first entries)
+        symload(kb + 2);
+    };
     auto block = [&](uint32_t kb) {
 #pragma unroll
         for (uint32_t j = 0; j < kDK; ++j) {
@@ -294,16 +305,16 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     };
 
     for (uint32_t k = 0; k < nbmax; ++k) {
-        lwrite(k + 4);  // into the slots of group k - 1, which no wave reads any more
-        gload(k + 5);
-        sbuild(k + 1);  // into the buffer of block k - 1 (the last steps of block k read its first entries)
-        symload(k + 2);
+        const uint32_t rem = k < nb ? nst - k * kDK : 0u;
+        const bool full = k < nb && rem >= kDK;
+        // (issuing this work between the block's steps instead measured the same: 0.1940 against
+        // 0.1934 ms; the per-block cost is the barrier and its LDS drain, profiles/r06_diag/)
+        blockwork(k);
         if (k < nb) {
-            const uint32_t rem = nst - k * kDK;
 #ifdef SVH_DIAG_SIMPLE  // diagnostics: every block through the plain steps (no software pipeline)
             tail(k, rem >= kDK ? kDK : rem);
 #else
-            if (rem >= kDK) block(k);
+            if (full) block(k);
             else tail(k, rem);
 #endif
         }

@@ -1093,7 +1093,12 @@ Model::Model(const HostModel& h, const svh_model_opts* opts) : host(h) {
             // diagonal plan (diag.hip): the scores-only batches the latency plan would take (DESIGN.md
             // 5l); SVH_DIAG=0 disables it, SVH_DIAG_MAX_NSEQ overrides the bound
             if (pipe.view.dtab && !(std::getenv("SVH_DIAG") && std::atoi(std::getenv("SVH_DIAG")) == 0)) {
-                diag_max_nseq = pipe_max_nseq;
+                // while its whole grid is resident at two workgroups per CU (its LDS allows two):
+                // beyond that the latency plan's two-per-CU regime is faster (2405.chmm: 52 sequences;
+                // at 64 the diagonal plan takes 0.296 ms against 0.303, at 90 0.363 against 0.313,
+                // profiles/r06_diag/widths.log)
+                const uint32_t w = diag_waves_for(4);
+                diag_max_nseq = std::min<uint32_t>(pipe_max_nseq, w * (2 * cu_count / pipe.plan.nrng));
                 if (const char* e = std::getenv("SVH_DIAG_MAX_NSEQ")) diag_max_nseq = (uint32_t)std::atoi(e);
             }
         }

@@ -86,7 +86,10 @@ def test_pipe_auto_selects_pipe_for_small_batches():
     assert info["pipe_slots"] > 0 and info["pipe_groups"] > 1
     small = model.batch(random_seqs(20, [50] * 4, seed=1))
     assert small.plan()["kernel"] == _lib.SVH_KERNEL_DIAG  # the latency plan's range: the diagonal plan
-    assert info["diag_max_nseq"] == info["pipe_max_nseq"], info
+    # the diagonal plan while its grid is resident at two workgroups per CU, the latency plan above
+    assert info["diag_max_nseq"] == min(info["pipe_max_nseq"], 4 * (2 * info["cu_count"] // info["diag_ranges"])), info
+    mid = model.batch(random_seqs(20, [8] * (info["diag_max_nseq"] + 1), seed=4))
+    assert mid.plan()["kernel"] == _lib.SVH_KERNEL_PIPE
     forced = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_PIPE).batch(random_seqs(20, [50] * 4, seed=1))
     assert forced.plan()["kernel"] == _lib.SVH_KERNEL_PIPE
     wide = model.batch(random_seqs(20, [8] * (info["pipe_max_nseq"] + 1), seed=2))

@@ -64,22 +64,29 @@ def test_scope_covers_every_model_and_geometry(scope):
 
 @pytest.mark.parametrize("name", MODELS)
 def test_scope_scores_and_paths(name, scope, emit3):
-    """Every emit_3 row of this model: scores and best states on one AUTO batch (the latency plan,
-    G named), then every row's decoded path; no row may fall back to the serial kernel."""
+    """Every emit_3 row of this model: scores and best states on one AUTO batch (the diagonal plan,
+    its ranges named) and on the latency plan forced (G named), then every row's decoded path (AUTO:
+    the latency plan's path variant); no row may fall back to the serial kernel."""
     hmm = svh.read_HMM(chmm(name))
     ref = scope["models"][name]
+    forced = svh.DeviceModel(hmm, kernel=_lib.SVH_KERNEL_PIPE)
     model = svh.DeviceModel(hmm)
-    batch = model.batch(emit3)
-    plan = batch.plan()
-    assert plan["kernel"] == _lib.SVH_KERNEL_PIPE, plan
-    assert plan["pipe_groups"] == expected_groups(hmm.states_num), plan
-    batch.run()
-    scores, best = batch.read()
-    assert batch.fallbacks() == 0
-    for q in range(len(emit3)):
-        assert sha(scores[q], np.float32) == ref[q]["scores_sha256"], (name, q)
-        assert int(best[q]) == ref[q]["best_state"], (name, q, int(best[q]), ref[q]["best_state"])
-    batch.close()
+    for m, kern in ((model, _lib.SVH_KERNEL_DIAG), (forced, _lib.SVH_KERNEL_PIPE)):
+        batch = m.batch(emit3)
+        plan = batch.plan()
+        assert plan["kernel"] == kern, plan
+        if kern == _lib.SVH_KERNEL_PIPE:
+            assert plan["pipe_groups"] == expected_groups(hmm.states_num), plan
+        else:
+            assert plan["diag_ranges"] == -(-(hmm.states_num - 2) // 64), plan
+        batch.run()
+        scores, best = batch.read()
+        assert batch.fallbacks() == 0
+        for q in range(len(emit3)):
+            assert sha(scores[q], np.float32) == ref[q]["scores_sha256"], (name, q, kern)
+            assert int(best[q]) == ref[q]["best_state"], (name, q, int(best[q]), ref[q]["best_state"])
+        batch.close()
+    forced.close()
     pbatch = model.batch(emit3, paths=True)
     pbatch.run()
     ps, pb, paths = pbatch.read(want_paths=True)

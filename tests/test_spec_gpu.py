@@ -66,8 +66,9 @@ def test_spec_level2_2405_emit50_config4():
     reference's interface (HIP_spec_impl; reference GraphBLAS_spec_impl.cpp:15-36, :68-80; the
     chunks' products evaluated on chip, nothing precomputed: the pipelined plan, pipe_l2.hip).
     All 50 sequences run in one batch and every row is compared bit-exact against the oracle's
-    level-2 scores (the oracle forms the 400 dense 2407 x 2408 products, 9.3 GB): rows 0..1 against the committed vectors, all 50 against the SHA-256 digests of
-    the oracle's float32 rows (tests/golden/make_golden.py spec2); every row also within the
+    level-2 scores (computed offline by the oracle, which does form the products): rows 0..1
+    against the committed vectors, all 50 against the SHA-256 digests of the oracle's float32 rows
+    (tests/golden/make_golden.py spec2); every row also within the
     reference's semantic-equality bound (HMM::almost_equal, |diff| <= 1) of the non-spec scores."""
     import hashlib
 

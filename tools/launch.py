@@ -34,6 +34,7 @@ def main():
     p.add_argument("--level", type=int, default=0)
     p.add_argument("--paths", action="store_true")
     p.add_argument("--nseq", type=int, default=0, help="use the first NSEQ sequences (0: all)")
+    p.add_argument("--kernel", default="auto", help="svh_model_opts.kernel: auto, pipe, pipew, diag, chain")
     a = p.parse_args()
     hmm = svh.read_HMM(os.path.join(ROOT, "data", "chmm_files", a.model))
     seqs = svh.read_emit_seq(os.path.join(ROOT, "data", "ess_files", a.ess))
@@ -43,7 +44,9 @@ def main():
                              for _ in range(a.replicate - 1) for s in seqs]
     if a.nseq:
         seqs = list(seqs)[: a.nseq]
-    model = svh.DeviceModel(hmm, device=0)
+    kern = {"auto": svh._lib.SVH_KERNEL_AUTO, "pipe": svh._lib.SVH_KERNEL_PIPE, "pipew": svh._lib.SVH_KERNEL_PIPE_WIDE,
+            "diag": svh._lib.SVH_KERNEL_DIAG, "chain": svh._lib.SVH_KERNEL_CHAIN}[a.kernel]
+    model = svh.DeviceModel(hmm, device=0, kernel=kern)
     if a.level >= 2:
         model.spec_build(a.level)
     batch = model.batch(seqs, paths=a.paths)
