@@ -124,7 +124,9 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
 
     const uint8_t* __restrict__ sym = b.symbols + (real ? b.sym_off[q] : 0);
     const uint32_t len = real ? (uint32_t)uniform((int)b.end[q]) : 0u;
-    const uint32_t nst = len > 1 ? len - 1 : 0u;  // steps: observations 1 .. len-1
+    const uint32_t beg = real ? (uint32_t)uniform((int)b.begin[q]) : 0u;
+    const uint32_t first = beg ? beg : 1u;                // first observation the steps run (state at first-1)
+    const uint32_t nst = len > first ? len - first : 0u;  // steps: observations first .. len-1
     const uint32_t nb = (nst + kDK - 1) / kDK;
     if (lane == 0) {
         wnb[w] = nb;
@@ -164,11 +166,11 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
             }
         }
     };
-    // ---- per-wave stream of block kb (steps 32 kb + 1 + j): lane j builds entry j from the symbol
-    // it loaded one block earlier
+    // ---- per-wave stream of block kb (steps kDK kb + 1 + j, step i reading observation first - 1 + i):
+    // lane j builds entry j from the symbol it loaded one block earlier
     uint32_t symv = 0;
     auto symload = [&](uint32_t kb) {
-        const uint32_t t = kb * kDK + 1 + lane;
+        const uint32_t t = first + kb * kDK + lane;
         const uint32_t tc = t < len ? t : (len ? len - 1 : 0u);
         symv = (real && lane < kDK) ? (uint32_t)sym[tc] : 0u;
     };
@@ -200,15 +202,21 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     sbuild(0);
     symload(1);
 
-    // ---- state at observation 0
+    // ---- state at observation first - 1
     float xv = kInf, F = kInf, c = kInf;
     uint32_t viol = 0;
-    if (real) {
+    if (real && beg == 0) {
         const uint32_t o0 = (uint32_t)uniform((int)sym[0]);
         const uint32_t p = rg * 64 + lane;
         xv = m.e0[(size_t)o0 * P + p] + m.start[p];
         F = m.rowF >= 0 ? m.hc[o0 * 8 + 5] + m.startF : kInf;
         c = (rg == 0 && lane == 0 && m.rowS >= 0) ? m.hc[o0 * 8 + 6] + m.startS : kInf;
+    } else if (real) {  // resumed row (the _spec tail, time-parallel segments): scores of first-1
+        const float* vin = b.v_in + (size_t)b.v_in_row[q] * m.n;
+        const uint32_t r = m.lrow[rg * 64 + lane];
+        xv = r != kNoRow ? vin[r] : kInf;
+        F = m.rowF >= 0 ? vin[m.rowF] : kInf;
+        c = (rg == 0 && lane == 0 && m.rowS >= 0) ? vin[m.rowS] : kInf;
     }
     __syncthreads();  // ring groups 0..3, wnb
     uint32_t nbmax = 0;
@@ -413,7 +421,7 @@ size_t diag_lds_bytes(uint32_t W, uint32_t S, uint32_t P) {
 
 hipError_t launch_diag(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream) {
     if (!m.dtab || m.nrng == 0 || m.SM != 2 || m.S == 0 || m.S > kDMaxSym || (size_t)m.nrng * 64 > m.P || m.wide ||
-        b.v_in || b.cmask || !x.part || !x.done || !x.viol || b.nseq > x.rows || x.G < m.nrng)
+        b.cmask || b.run_mask || (b.v_in && !b.v_in_row) || !x.part || !x.done || !x.viol || b.nseq > x.rows || x.G < m.nrng)
         return hipErrorInvalidValue;
     if (b.nseq == 0) return hipSuccess;
     const uint32_t W = diag_waves_for(b.nseq);

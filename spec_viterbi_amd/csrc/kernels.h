@@ -306,7 +306,7 @@ inline size_t pipe_path_lds_bytes(uint32_t W) { return (size_t)W * 8 * kPQuadStr
 // (position, observation) grid -- lane l of range r holds position (64 r + l + i) mod (64 nrng) after
 // step i, so a position's chain input is the lane's own previous score (no exchange between waves).
 // A workgroup is diag_waves_for(nseq) sequences x one range; rows whose speculation fails are re-run
-// in the same launch.  Scores only, rows from observation 0 (b.v_in null).
+// in the same launch.  Scores only; a row starts at observation 0 or resumes at begin > 0 from v_in.
 uint32_t diag_waves_for(uint64_t nseq);
 size_t diag_lds_bytes(uint32_t W, uint32_t S, uint32_t P);
 hipError_t launch_diag(const PipeModel& m, const FusedBatch& b, const PipeScratch& x, hipStream_t stream);

@@ -1814,15 +1814,22 @@ void Batch::run(uint32_t level, hipStream_t s) {
     }
     pipe_ran = false;
     l2_ran = false;
-    if (const DevicePipePlan* dp = paths || level >= 2 ? nullptr : model->diag_for(nseq)) {  // diagonal plan: scratch
+    // (level >= 2: the chunks run elsewhere; the tail, rows resumed from the chunks' scores, runs on
+    // the diagonal plan when it has one for this batch -- the scratch then covers both plans)
+    const DevicePipePlan* dp = paths ? nullptr : model->diag_for(nseq);
+    if (dp && level <= 1) {  // diagonal plan: scratch
         pipe.ensure(nseq, dp->plan.nrng, s);
         fb.pipe = &pipe.view;
         pipe_ran = true;
     } else if (const DevicePipePlan* pp = paths ? nullptr : model->pipe_for(nseq)) {  // pipelined plan: scratch
-        pipe.ensure(nseq, pp->plan.G, s);
+        pipe.ensure(nseq, std::max<uint32_t>(pp->plan.G, dp ? dp->plan.nrng : 0u), s);
         pipe.note_launch(s);
         fb.pipe = &pipe.view;
-        pipe_ran = model->band_for(false, nseq) != nullptr;  // launch_steps' condition
+        pipe_ran = dp || model->band_for(false, nseq) != nullptr;  // launch_steps' condition
+    } else if (dp) {
+        pipe.ensure(nseq, dp->plan.nrng, s);
+        fb.pipe = &pipe.view;
+        pipe_ran = true;
     }
     auto launch_step_kernel = [&](const FusedBatch& b, bool want_paths) { model->launch_steps(b, want_paths, s); };
 
@@ -2279,7 +2286,7 @@ void Batch::read_async(hipStream_t s, float* scores, int64_t* best, int32_t* pat
 void Model::launch_steps(const FusedBatch& b, bool want_paths, hipStream_t s) const {
     const DevicePlan* dp = plan_for(want_paths);
     const DeviceBandPlan* bpl = band_for(want_paths, b.nseq);
-    const DevicePipePlan* dpl = want_paths || b.v_in ? nullptr : diag_for(b.nseq);
+    const DevicePipePlan* dpl = want_paths ? nullptr : diag_for(b.nseq);
     if (dpl && b.pipe && b.pipe->rows >= b.nseq && b.pipe->G >= dpl->plan.nrng) {
         // diagonal plan: rows whose speculation fails are re-run in the same launch
         hip_check(launch_diag(dpl->view, b, *b.pipe, s), "diagonal Viterbi kernel");

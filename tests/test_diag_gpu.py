@@ -236,3 +236,40 @@ def test_diag_two_batches_two_streams():
     a.close()
     b.close()
     model.close()
+
+
+@pytest.mark.parametrize("kern", [DIAG, _lib.SVH_KERNEL_AUTO])
+def test_diag_spec_tail_resumes_from_device_scores(kern):
+    """_spec level 2: the chunks run on the dense products (DIAG) or on the latency plan's level-2
+    kernel (AUTO); the tail -- rows resumed at begin > 0 from the chunks' device scores (v_in) -- on
+    the diagonal plan.  Tails of 0 and 1 observations, a length-1 row (no chunk); bit-exact against
+    the oracle's level-2 association.  (The level-2 rocprof trace, profiles/r06_m2, shows the tail's
+    diag_viterbi_kernel launch.)"""
+    hmm = svh.read_HMM(chmm("100.chmm"))
+    base = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    seqs = [base[0][:301], base[1][:64], base[2][:2], base[0][:1], base[1][:1000]]
+    model = svh.DeviceModel(hmm, kernel=kern)
+    model.spec_build(2)
+    batch = model.batch(seqs)
+    batch.run(2)
+    s, _ = batch.read()
+    batch.close()
+    model.close()
+    for q, seq in enumerate(seqs):
+        ref = oracle.viterbi_spec(hmm, 2, seq)
+        assert bit_equal(s[q], ref), (q, first_mismatch(s[q], ref))
+
+
+def test_diag_spec3_tail_equals_chain():
+    """_spec level 3 (tails of 0, 1 and 2 observations, one starting at 256) on the diagonal plan
+    against the serial chain kernel at level 3, bit-exact."""
+    hmm = svh.read_HMM(chmm("1001.chmm"))
+    base = svh.read_emit_seq(ess("emit_3_3500_20.ess"))
+    seqs = [base[0][:258], base[1][:259], base[2][:260], base[0][:3]]
+    out = []
+    for kern in (DIAG, _lib.SVH_KERNEL_CHAIN):
+        model = svh.DeviceModel(hmm, kernel=kern)
+        model.spec_build(3)
+        out.append(model.viterbi(seqs, level=3))
+        model.close()
+    assert_same(out[0][0], out[0][1], out[1][0], out[1][1])

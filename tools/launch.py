@@ -7,7 +7,8 @@ prints one JSON line with the mean HIP-event time per pass.  Output is checked b
 the committed digests of all 50 rows of 2405.chmm x emit_50_3500_20 when that is the workload.
 
     python3 tools/launch.py [--model 2405.chmm] [--ess emit_50_3500_20.ess] [--replicate R]
-                            [--steps K] [--warmup W] [--level L] [--paths]
+                            [--steps K] [--warmup W] [--level L] [--paths] [--nseq N] [--maxlen M]
+                            [--kernel auto|pipe|pipew|diag|chain]
 """
 from __future__ import annotations
 
@@ -34,6 +35,7 @@ def main():
     p.add_argument("--level", type=int, default=0)
     p.add_argument("--paths", action="store_true")
     p.add_argument("--nseq", type=int, default=0, help="use the first NSEQ sequences (0: all)")
+    p.add_argument("--maxlen", type=int, default=0, help="truncate every sequence to MAXLEN observations (0: as read)")
     p.add_argument("--kernel", default="auto", help="svh_model_opts.kernel: auto, pipe, pipew, diag, chain")
     a = p.parse_args()
     hmm = svh.read_HMM(os.path.join(ROOT, "data", "chmm_files", a.model))
@@ -44,6 +46,8 @@ def main():
                              for _ in range(a.replicate - 1) for s in seqs]
     if a.nseq:
         seqs = list(seqs)[: a.nseq]
+    if a.maxlen:
+        seqs = [s[: a.maxlen] for s in seqs]
     kern = {"auto": svh._lib.SVH_KERNEL_AUTO, "pipe": svh._lib.SVH_KERNEL_PIPE, "pipew": svh._lib.SVH_KERNEL_PIPE_WIDE,
             "diag": svh._lib.SVH_KERNEL_DIAG, "chain": svh._lib.SVH_KERNEL_CHAIN}[a.kernel]
     model = svh.DeviceModel(hmm, device=0, kernel=kern)
@@ -61,7 +65,7 @@ def main():
     # (diagnostic ablations, SVH_*_DEBUG or SVH_LAUNCH_NOCHECK=1 for ablation builds, give wrong
     # results by design: not checked)
     diag = any(os.environ.get(k) for k in ("SVH_PIPE_DEBUG", "SVH_BAND_DEBUG", "SVH_LAUNCH_NOCHECK"))
-    if a.model == "2405.chmm" and a.ess == "emit_50_3500_20.ess" and a.level <= 2 and not diag:
+    if a.model == "2405.chmm" and a.ess == "emit_50_3500_20.ess" and a.level <= 2 and not diag and not a.maxlen:
         import hashlib
 
         from tests.helpers import load_digests
