@@ -70,6 +70,19 @@ constexpr uint32_t kNS = kPS + 2;      // stream registers: entries j .. j + kPS
 static_assert(kPE < kPS && kPS % 2 == 0 && kDK % kNS == 0 && kDK % kPE == 0,
               "prefetch distances: the register slots of step j (j % kNS, j % kPE) repeat every block");
 constexpr uint32_t kDMaxSym = 32;
+// SVH_DIAG_AB (diagnostic builds, timing only, wrong results): 1 = no stream reads in the steps
+// (every step takes the block's first entry), 2 = no ring reads (the prologue's pairs), 3 = no
+// barrier between blocks, 4 = no prologue table loads, 5 = no partials / combine, 6 = return at entry,
+// 7 = no arrival count (the last range combines), 8 = the arrival count without the combine
+#ifndef SVH_DIAG_AB
+#define SVH_DIAG_AB 0
+#endif
+#ifndef SVH_DIAG_FINISH
+#define SVH_DIAG_FINISH 0
+#endif
+#ifndef SVH_DIAG_DONE_STRIDE  // words between rows' arrival counts (the scratch holds 32 per row)
+#define SVH_DIAG_DONE_STRIDE 1
+#endif
 
 __device__ __forceinline__ f2 lds_ld2(uint32_t a) {
     return *(const __attribute__((address_space(3))) f2*)(size_t)a;
@@ -188,6 +201,10 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     };
 
     // ---- prologue: groups 0..3 in the ring, group 4 in flight; the stream of block 0
+#if SVH_DIAG_AB == 6  // diagnostics: the launch alone
+    return;
+#endif
+#if SVH_DIAG_AB != 4  // diagnostics: no prologue table loads (rows of one observation stay exact)
     gload(0);
     lwrite(0);
     gload(1);
@@ -197,6 +214,7 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     gload(3);
     lwrite(3);
     gload(4);
+#endif
     symload(0);
     __syncthreads();  // the symbol template
     sbuild(0);
@@ -272,12 +290,6 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
         XP.x = fminf(zb, za);
         FC = (f2){Wv.x, cn};
     };
-    // SVH_DIAG_AB (diagnostic builds, timing only, wrong results): 1 = no stream reads in the steps
-    // (every step takes the block's first entry), 2 = no ring reads (the prologue's pairs), 3 = no
-    // barrier between blocks
-#ifndef SVH_DIAG_AB
-#define SVH_DIAG_AB 0
-#endif
     auto blockwork = [&](uint32_t kb) {
         lwrite(kb + 4);  // into the slots of group kb - 1, which no wave reads any more
         gload(kb + 5);
@@ -334,6 +346,34 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
     xv = XP.x;
 
     // ---- scores of the light positions and this wave's partials
+#if SVH_DIAG_AB == 5  // diagnostics: the scores only (every wave leaves here)
+    if (real && m.lrow[(rg * 64 + lane + nst) % NP] != kNoRow)
+        g_st_score(b.scores + (size_t)q * m.n + m.lrow[(rg * 64 + lane + nst) % NP], xv);
+    return;
+#endif
+#if SVH_DIAG_FINISH  // partials only: diag_finish_kernel combines them after this launch
+    if (real) {
+        float* out = b.scores + (size_t)q * m.n;
+        const uint32_t r = m.lrow[(rg * 64 + lane + nst) % NP];
+        float bv = kInf;
+        uint32_t bk = kNoRow;
+        if (r != kNoRow) {
+            out[r] = xv;
+            bv = xv;
+            bk = r;
+        }
+        wave_lexmin63(bv, bk);
+        const float cmin = wave_min63(c);
+        const bool any_viol = __builtin_amdgcn_ballot_w64(viol != 0) != 0;
+        if (lane == 63) {
+            uint64_t* part = x.part + ((size_t)q * x.G + rg) * 2;
+            part[0] = ((uint64_t)(any_viol ? 1u : 0u) << 32) | __builtin_bit_cast(uint32_t, cmin);
+            part[1] = lex_key(bv, bk);
+            if (rg == 0 && m.rowF >= 0) out[m.rowF] = F;
+        }
+    }
+    return;
+#endif
     uint32_t last = 0;
     if (real) {
         float* out = b.scores + (size_t)q * m.n;
@@ -353,9 +393,16 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
             uint64_t* part = x.part + ((size_t)q * x.G + rg) * 2;
             g_st64(part, ((uint64_t)(any_viol ? 1u : 0u) << 32) | __builtin_bit_cast(uint32_t, cmin));
             g_st64(part + 1, lex_key(bv, bk));
+#if SVH_DIAG_AB == 7  // diagnostics: no arrival count (the last range combines, unordered)
+            last = rg == NR - 1 ? 1u : 0u;
+#else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint32_t d = __hip_atomic_fetch_add(x.done + q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t d = __hip_atomic_fetch_add(x.done + (size_t)q * SVH_DIAG_DONE_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             last = d == NR - 1 ? 1u : 0u;
+#endif
+#if SVH_DIAG_AB == 8  // diagnostics: the arrival count, no combine
+            last = 0;
+#endif
         }
         last = readlane_u(last, 63);
     }
@@ -384,7 +431,7 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
             }
             if (b.best) b.best[q] = bk2 == kNoRow ? -1 : (int64_t)bk2;
             x.viol[q] = any ? 1u : 0u;
-            __hip_atomic_store(x.done + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(x.done + (size_t)q * SVH_DIAG_DONE_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (any) rrow[w] = q;
         }
     }
@@ -401,6 +448,42 @@ void diag_viterbi_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
             pipe_rerun_row<2, W, SX>(m, b, rq[u], lds);
         }
     }
+}
+
+// One workgroup per row after the main launch: the row's NR partials -> S, best state, the
+// violation flag; a row whose speculation failed is re-run here exactly (pipe_rerun_row).
+template <bool SX>
+__global__ __launch_bounds__(256) void diag_finish_kernel(PipeModel m, FusedBatch b, PipeScratch x) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
+    uint32_t* flag = reinterpret_cast<uint32_t*>(lds + 2 * (size_t)m.P + 8);
+    if (tid < 64) {
+        float C = kInf, bv = kInf;
+        uint32_t bk = kNoRow, vi = 0;
+        for (uint32_t u = lane; u < m.nrng; u += 64) {
+            const uint64_t* pu = x.part + ((size_t)q * x.G + u) * 2;
+            const uint64_t a = pu[0], k2 = pu[1];
+            C = fminf(C, __builtin_bit_cast(float, (uint32_t)a));
+            vi |= (uint32_t)(a >> 32);
+            if (k2 != ~0ull) lex_min(bv, bk, lex_key_value(k2), lex_key_index(k2));
+        }
+        C = wave_min63(C);
+        wave_lexmin63(bv, bk);
+        const bool any = __builtin_amdgcn_ballot_w64(vi != 0) != 0;
+        if (lane == 63) {
+            float* out = b.scores + (size_t)q * m.n;
+            if (m.rowF >= 0) lex_min(bv, bk, out[m.rowF], (uint32_t)m.rowF);
+            if (m.rowS >= 0) {
+                out[m.rowS] = C;
+                lex_min(bv, bk, C, (uint32_t)m.rowS);
+            }
+            if (b.best) b.best[q] = bk == kNoRow ? -1 : (int64_t)bk;
+            x.viol[q] = any ? 1u : 0u;
+            *flag = any ? 1u : 0u;
+        }
+    }
+    __syncthreads();
+    if (*flag) pipe_rerun_row<2, 4, SX>(m, b, q, lds);
 }
 
 template <int W>
@@ -448,7 +531,15 @@ hipError_t launch_diag(const PipeModel& m, const FusedBatch& b, const PipeScratc
     FusedBatch bb = b;
     PipeScratch xx = x;
     void* args[] = {&mm, &bb, &xx};
-    return hipLaunchKernel(fn, dim3((uint32_t)grid), dim3(64 * W), args, lds, stream);
+    const hipError_t e = hipLaunchKernel(fn, dim3((uint32_t)grid), dim3(64 * W), args, lds, stream);
+#if SVH_DIAG_FINISH
+    if (e != hipSuccess) return e;
+    const void* fin = m.sx ? reinterpret_cast<const void*>(&diag_finish_kernel<true>)
+                           : reinterpret_cast<const void*>(&diag_finish_kernel<false>);
+    return hipLaunchKernel(fin, dim3(b.nseq), dim3(256), args, (2 * (size_t)m.P + 8 + 1) * 4, stream);
+#else
+    return e;
+#endif
 }
 
 }  // namespace svh

@@ -946,7 +946,7 @@ void PipeScratchBuffers::ensure(uint32_t rows, uint32_t G, hipStream_t s) {
         d.alloc(bytes);
         hip_check(hipMemsetAsync(d.ptr, 0, d.bytes, s), "pipe scratch");
     };
-    zeroed(d_done, (size_t)rows * 4);
+    zeroed(d_done, (size_t)rows * 128);  // (one 128-byte line per row: diag.hip SVH_DIAG_DONE_STRIDE)
     zeroed(d_part, (size_t)rows * G * 16);
     zeroed(d_gran, (size_t)rows * std::max<uint32_t>(G - 1, 1) * kPipeGRing * 8);
     zeroed(d_cons, (size_t)rows * G * 8);
